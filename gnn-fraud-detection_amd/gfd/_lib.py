@@ -1,0 +1,90 @@
+"""ctypes binding of libgfd.so (include/gfd.h).  Fails loudly when missing.
+
+There is deliberately no fallback: if the HIP library cannot be loaded, every
+``gfd`` op raises ``RuntimeError`` -- the product path never silently runs a
+CPU or PyTorch restatement.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import threading
+
+_LIB = None
+_LOCK = threading.Lock()
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgfd.so")
+
+c_i32, c_i64, c_u64, c_f32, c_sz = ct.c_int32, ct.c_int64, ct.c_uint64, ct.c_float, ct.c_size_t
+P = ct.c_void_p
+
+# name -> (restype, argtypes); mirrors include/gfd.h one to one
+SIGNATURES = {
+    "gfd_status_string": (ct.c_char_p, [c_i32]),
+    "gfd_abi_version": (ct.c_int, []),
+    "gfd_csr_workspace_size": (c_sz, [c_i64, c_i64]),
+    "gfd_csr_from_coo": (c_i32, [P, c_i64, c_i64, P, P, P, c_sz, P]),
+    "gfd_csc_workspace_size": (c_sz, [c_i64, c_i64]),
+    "gfd_csc_from_csr": (c_i32, [P, P, c_i64, c_i64, P, P, P, P, c_sz, P]),
+    "gfd_plan_workspace_size": (c_sz, [c_i64]),
+    "gfd_plan_hubs": (c_i32, [P, c_i64, c_i32, c_i32, P, P, P, P, c_i64, c_i64,
+                              ct.POINTER(c_i64), ct.POINTER(c_i64), P, c_sz, P]),
+    "gfd_gat_packed_size": (c_sz, [ct.c_int, ct.c_int, ct.c_int]),
+    "gfd_gat_pack_weights": (c_i32, [P, P, P, ct.c_int, ct.c_int, ct.c_int, P, P]),
+    "gfd_gat_logits": (c_i32, [P, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),
+    "gfd_gat_fwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int, c_i64,
+                                          c_i64]),
+    "gfd_gat_aggregate": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P, P, P,
+                                  ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, c_i64,
+                                  c_i64, ct.c_int, P, P, P, c_sz, P]),
+    "gfd_gat_fwd": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int, ct.c_int,
+                            c_f32, c_f32, c_u64, P, P, P, P, c_i64, c_i64, P, P, P, P, c_sz, P]),
+    "gfd_gat_bwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int]),
+    "gfd_gat_bwd": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, P, ct.c_int,
+                            ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, P, P, P, P, P, c_sz, P]),
+}
+
+STATUS = {0: "ok", 1: "invalid argument", 2: "edge index out of range", 3: "workspace too small",
+          4: "HIP runtime error", 5: "unsupported configuration"}
+
+
+class GfdError(RuntimeError):
+    def __init__(self, fn: str, status: int):
+        self.status = status
+        super().__init__(f"{fn} failed: {STATUS.get(status, status)} (gfd_status={status})")
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes library. Raises if it is missing."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is None:
+            if not os.path.exists(path):
+                raise RuntimeError(
+                    f"libgfd.so not found at {path}: build it with `python -m gfd.build` "
+                    "(gnn-fraud-detection_amd/) or __graft_entry__.build(). gfd has no CPU fallback.")
+            lib = ct.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _LIB = lib
+    return _LIB
+
+
+def call(name: str, *args):
+    st = getattr(load(), name)(*args)
+    if st != 0:
+        raise GfdError(name, st)
+    return st
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,159 @@
+"""Device graph format: COO edge_index -> cached destination-sorted CSR.
+
+The reference hands GATConv a COO ``edge_index`` (``LongTensor [2, E]``,
+dataset.py:104) and PyG rebuilds the self-loop-normalised edge list on every
+call and every layer (remove_self_loops + add_self_loops inside
+GATConv.forward).  Here the CSR (int32 ``rowptr[N+1]`` / ``col[E']``, loops
+removed then one appended per node, duplicates kept, stable order) is built
+once on the GPU by ``gfd_csr_from_coo`` and cached per
+``(edge_index storage, version, N)``; the source-sorted CSC view used by the
+backward and the hub plan (rows with more than ``hub_threshold`` messages are
+split into chunks) are derived lazily from it.
+"""
+from __future__ import annotations
+
+import os
+import weakref
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+HUB_THRESHOLD = int(os.environ.get("GFD_HUB_THRESHOLD", "128"))
+HUB_CHUNK = int(os.environ.get("GFD_HUB_CHUNK", "128"))
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+@dataclass
+class HubPlan:
+    hub_rank: torch.Tensor
+    hub_chunk: Optional[torch.Tensor]
+    hub_chunk_ptr: Optional[torch.Tensor]
+    hub_dst: Optional[torch.Tensor]
+    num_hubs: int
+    num_chunks: int
+
+    def args(self):
+        if self.num_hubs == 0:
+            return (None, None, None, None, 0, 0)
+        return (self.hub_rank.data_ptr(), self.hub_chunk.data_ptr(), self.hub_chunk_ptr.data_ptr(),
+                self.hub_dst.data_ptr(), self.num_hubs, self.num_chunks)
+
+
+def plan_hubs(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
+              chunk: int = HUB_CHUNK) -> HubPlan:
+    """Hub plan for the destination range described by ``rowptr`` ([n+1] int32)."""
+    n = rowptr.numel() - 1
+    dev = rowptr.device
+    max_hubs = num_messages // (threshold + 1) + 1
+    max_chunks = num_messages // chunk + max_hubs + 1
+    hub_rank = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    hub_chunk = torch.empty(4 * max_chunks, dtype=torch.int32, device=dev)
+    hub_chunk_ptr = torch.empty(max_hubs + 1, dtype=torch.int32, device=dev)
+    hub_dst = torch.empty(max_hubs, dtype=torch.int32, device=dev)
+    ws = _ws(_lib.load().gfd_plan_workspace_size(n), dev)
+    nh, nc = _lib.c_i64(0), _lib.c_i64(0)
+    _lib.call("gfd_plan_hubs", rowptr.data_ptr(), n, threshold, chunk, hub_rank.data_ptr(),
+              hub_chunk.data_ptr(), hub_chunk_ptr.data_ptr(), hub_dst.data_ptr(), max_hubs,
+              max_chunks, _lib.ct.byref(nh), _lib.ct.byref(nc), ws.data_ptr(), ws.numel(),
+              _lib.stream_handle(dev))
+    return HubPlan(hub_rank, hub_chunk[:4 * nc.value], hub_chunk_ptr[:nh.value + 1],
+                   hub_dst[:nh.value], nh.value, nc.value)
+
+
+@dataclass
+class CSC:
+    colptr: torch.Tensor
+    dst: torch.Tensor
+    eid: torch.Tensor
+
+
+@dataclass
+class CSRGraph:
+    """Destination-sorted CSR with PyG's self-loop policy, plus lazy views."""
+    num_nodes: int
+    rowptr: torch.Tensor      # int32 [N+1]
+    col: torch.Tensor         # int32 [E'] (source ids)
+    num_messages: int         # E' = E - self loops + N
+    num_input_edges: int
+    _hubs: Optional[HubPlan] = field(default=None, repr=False)
+    _csc: Optional[CSC] = field(default=None, repr=False)
+
+    @property
+    def device(self):
+        return self.rowptr.device
+
+    def hubs(self) -> HubPlan:
+        if self._hubs is None:
+            self._hubs = plan_hubs(self.rowptr, self.num_messages)
+        return self._hubs
+
+    def csc(self) -> CSC:
+        if self._csc is None:
+            N, M = self.num_nodes, self.num_messages
+            colptr = torch.empty(N + 1, dtype=torch.int32, device=self.device)
+            dst = torch.empty(M, dtype=torch.int32, device=self.device)
+            eid = torch.empty(M, dtype=torch.int32, device=self.device)
+            ws = _ws(_lib.load().gfd_csc_workspace_size(M, N), self.device)
+            _lib.call("gfd_csc_from_csr", self.rowptr.data_ptr(), self.col.data_ptr(), M, N,
+                      colptr.data_ptr(), dst.data_ptr(), eid.data_ptr(), ws.data_ptr(),
+                      ws.numel(), _lib.stream_handle(self.device))
+            self._csc = CSC(colptr, dst, eid)
+        return self._csc
+
+    def shard(self, lo: int, hi: int) -> "CSRShard":
+        """Destination range [lo, hi): a rowptr view (absolute positions into col)."""
+        rp = self.rowptr[lo:hi + 1]
+        m = int(self.rowptr[hi].item()) - int(self.rowptr[lo].item())
+        return CSRShard(self, lo, hi, rp, plan_hubs(rp, m))
+
+
+@dataclass
+class CSRShard:
+    graph: CSRGraph
+    lo: int
+    hi: int
+    rowptr: torch.Tensor
+    hubs: HubPlan
+
+
+def csr_from_coo(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
+    """Build the CSR on the device of ``edge_index`` (validates indices)."""
+    if edge_index.dim() != 2 or edge_index.size(0) != 2:
+        raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+    if not edge_index.is_cuda:
+        raise RuntimeError("gfd graphs live on the GPU: move edge_index to a HIP device first")
+    ei = edge_index.to(torch.int64).contiguous()
+    E = ei.size(1)
+    dev = ei.device
+    rowptr = torch.empty(num_nodes + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(E + num_nodes, dtype=torch.int32, device=dev)
+    ws = _ws(_lib.load().gfd_csr_workspace_size(E, num_nodes), dev)
+    st = _lib.load().gfd_csr_from_coo(ei.data_ptr(), E, num_nodes, rowptr.data_ptr(),
+                                      col.data_ptr(), ws.data_ptr(), ws.numel(),
+                                      _lib.stream_handle(dev))
+    if st == 2:
+        raise IndexError(f"edge_index holds an index outside [0, {num_nodes})")
+    if st != 0:
+        raise _lib.GfdError("gfd_csr_from_coo", st)
+    M = int(rowptr[num_nodes].item())
+    return CSRGraph(num_nodes, rowptr, col[:M], M, E)
+
+
+_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def get_graph(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
+    """Cached ``csr_from_coo`` keyed on the tensor object, its version and N."""
+    key = (edge_index._version, int(num_nodes), edge_index.data_ptr(), tuple(edge_index.shape))
+    ent = _CACHE.get(edge_index)
+    if ent is not None and ent[0] == key:
+        return ent[1]
+    g = csr_from_coo(edge_index, num_nodes)
+    _CACHE[edge_index] = (key, g)
+    return g

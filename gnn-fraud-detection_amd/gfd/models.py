@@ -1,0 +1,106 @@
+"""Reference model families on the HIP GATConv.
+
+``GAT`` mirrors /root/reference/src/models/gat.py (ctor :14-58, forward
+:60-96, predict :98-122) and ``TemporalGNN`` mirrors
+/root/reference/src/models/tgn.py (ctor :18-63, forward :67-113) -- same
+constructor arguments, same submodule names (so ``results/gat_model.pt`` and
+``results/tgn_model.pt`` load with ``strict=True``), same outputs.  The only
+difference is the GATConv underneath: ``gfd.nn.GATConv`` (libgfd.so).
+
+The per-layer epilogue is the reference's: GATConv -> BatchNorm1d -> ReLU ->
+dropout -> residual when widths match (gat.py:79-91).
+
+``forward_snapshots`` is config C3: the TGN forward over per-time-step
+snapshots (h0 = 0 per step, tgn.py:88-89).  Elliptic edges never cross time
+steps, so the 49 snapshot forwards are one block-diagonal launch over the
+step-sorted graph; the result equals the per-step forwards exactly in eval
+mode (checked against the reference in tests/golden).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .nn import GATConv
+
+
+class _GATStack(nn.Module):
+    """The GATConv/BN/ReLU/dropout/residual stack shared by both families."""
+
+    def __init__(self, in_channels: int, hidden_channels: int, out_channels: int,
+                 num_layers: int = 2, dropout: float = 0.2, residual: bool = True,
+                 use_batch_norm: bool = True):
+        super().__init__()
+        self.in_channels, self.hidden_channels = in_channels, hidden_channels
+        self.out_channels, self.num_layers = out_channels, num_layers
+        self.dropout, self.residual, self.use_batch_norm = dropout, residual, use_batch_norm
+        # layer 0 takes in_channels, every later layer hidden_channels (gat.py:39-56)
+        widths = [in_channels] + [hidden_channels] * max(num_layers - 1, 0)
+        self.gat_layers = nn.ModuleList(
+            GATConv(w, hidden_channels, heads=8, concat=False, dropout=dropout) for w in widths)
+        self.batch_norms = (nn.ModuleList(nn.BatchNorm1d(hidden_channels) for _ in widths)
+                            if use_batch_norm else None)
+
+    def encode(self, x: torch.Tensor, edge_index) -> torch.Tensor:
+        h = x
+        for layer, conv in enumerate(self.gat_layers):
+            y = conv(h, edge_index)
+            if self.batch_norms is not None:
+                y = self.batch_norms[layer](y)
+            y = F.dropout(F.relu(y), p=self.dropout, training=self.training)
+            h = h + y if (self.residual and h.size(-1) == y.size(-1)) else y
+        return h
+
+
+class GAT(_GATStack):
+    """Drop-in for ``src.models.gat.GAT``."""
+
+    def __init__(self, in_channels: int, hidden_channels: int, out_channels: int,
+                 num_layers: int = 2, dropout: float = 0.2, residual: bool = True,
+                 use_batch_norm: bool = True):
+        super().__init__(in_channels, hidden_channels, out_channels, num_layers, dropout,
+                         residual, use_batch_norm)
+        self.out = nn.Linear(hidden_channels, out_channels)
+
+    def forward(self, x, edge_index, batch: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self.out(self.encode(x, edge_index))
+
+    def predict(self, x, edge_index, batch=None, apply_sigmoid: bool = True) -> torch.Tensor:
+        out = self.forward(x, edge_index, batch)
+        return torch.sigmoid(out) if apply_sigmoid else out
+
+
+class TemporalGNN(_GATStack):
+    """Drop-in for ``src.models.tgn.TemporalGNN``: GAT stack -> GRUCell -> Linear."""
+
+    def __init__(self, in_channels: int, hidden_channels: int, out_channels: int,
+                 num_layers: int = 2, dropout: float = 0.2, residual: bool = True,
+                 use_batch_norm: bool = True):
+        super().__init__(in_channels, hidden_channels, out_channels, num_layers, dropout,
+                         residual, use_batch_norm)
+        self.gru = nn.GRUCell(hidden_channels, hidden_channels)
+        self.out = nn.Linear(hidden_channels, out_channels)
+
+    def forward(self, x, edge_index, batch: Optional[torch.Tensor] = None,
+                hidden_state: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        if hidden_state is None:
+            hidden_state = x.new_zeros((x.size(0), self.hidden_channels))
+        new_hidden = self.gru(self.encode(x, edge_index), hidden_state)
+        return self.out(new_hidden), new_hidden
+
+    def predict(self, x, edge_index, batch=None, hidden_state=None,
+                apply_sigmoid: bool = True) -> torch.Tensor:
+        out, _ = self.forward(x, edge_index, batch, hidden_state)
+        return torch.sigmoid(out) if apply_sigmoid else out
+
+    def forward_snapshots(self, x: torch.Tensor, edge_index: torch.Tensor,
+                          time_step: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Config C3: per-time-step snapshot forwards (h0 = 0 each step) in one
+        launch.  Requires every edge to join two nodes of the same step (true
+        for Elliptic); raises otherwise."""
+        if (time_step[edge_index[0]] != time_step[edge_index[1]]).any():
+            raise ValueError("forward_snapshots: an edge crosses time steps")
+        return self.forward(x, edge_index)

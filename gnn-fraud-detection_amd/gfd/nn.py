@@ -1,0 +1,169 @@
+"""Drop-in ``GATConv`` on the HIP library.
+
+Replaces ``from torch_geometric.nn import GATConv`` at
+/root/reference/src/models/gat.py:4 and tgn.py:4.  Same constructor subset as
+the reference uses (``GATConv(in, out, heads=8, concat=False, dropout=p)``,
+gat.py:39,45,51; tgn.py:43,49,55), same call (``conv(x, edge_index)``,
+gat.py:80, tgn.py:94), same parameters and state-dict keys as PyG 2.x for an
+int ``in_channels``: ``lin_src.weight [H*C, F]`` with ``lin_dst`` the same
+module (both keys saved and accepted), ``att_src``/``att_dst [1, H, C]``,
+``bias [C]`` -- the shipped checkpoints load with ``strict=True``.
+
+Forward and backward both run in libgfd.so (``gfd_gat_fwd`` /
+``gfd_gat_bwd``); there is no CPU or eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .graph import CSRGraph, _ws, get_graph
+
+SUPPORTED_HEADS = 8
+SUPPORTED_CHANNELS = 64
+
+
+def _check_tensor(name: str, t: torch.Tensor, device):
+    if not t.is_cuda:
+        raise RuntimeError(f"gfd GATConv: {name} must be on a HIP device (got {t.device})")
+    if t.device != device:
+        raise RuntimeError(f"gfd GATConv: {name} is on {t.device}, expected {device}")
+    if t.dtype != torch.float32:
+        raise TypeError(f"gfd GATConv: {name} must be float32 (got {t.dtype})")
+
+
+class GATConvFunction(torch.autograd.Function):
+    """autograd.Function around gfd_gat_fwd / gfd_gat_bwd."""
+
+    @staticmethod
+    def forward(ctx, x, weight, att_src, att_dst, bias, graph: CSRGraph, negative_slope: float,
+                dropout_p: float, seed: int):
+        dev = x.device
+        for n, t in (("x", x), ("weight", weight), ("att_src", att_src), ("att_dst", att_dst)):
+            _check_tensor(n, t, dev)
+        if bias is not None:
+            _check_tensor("bias", bias, dev)
+        x = x.contiguous()
+        weight = weight.contiguous()
+        att_src = att_src.contiguous()
+        att_dst = att_dst.contiguous()
+        N, F = x.shape
+        HC = weight.size(0)
+        H, C = SUPPORTED_HEADS, HC // SUPPORTED_HEADS
+        hubs = graph.hubs()
+        need_stats = any(ctx.needs_input_grad[:5])
+        out = torch.empty((N, C), dtype=torch.float32, device=dev)
+        st = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
+        stats = torch.empty((N, 2 * H), dtype=torch.float32, device=dev) if need_stats else None
+        lib = _lib.load()
+        ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, hubs.num_hubs, hubs.num_chunks), dev)
+        _lib.call("gfd_gat_fwd", x.data_ptr(), N, F, F, graph.rowptr.data_ptr(),
+                  graph.col.data_ptr(), weight.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(),
+                  _lib.ptr(bias), H, C, float(negative_slope), float(dropout_p),
+                  int(seed) & (2 ** 64 - 1), *hubs.args(), out.data_ptr(), st.data_ptr(),
+                  _lib.ptr(stats), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+        if need_stats:
+            ctx.save_for_backward(x, weight, att_src, att_dst, st, stats)
+            ctx.graph = graph
+            ctx.meta = (float(negative_slope), float(dropout_p), int(seed), bias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, weight, att_src, att_dst, st, stats = ctx.saved_tensors
+        graph: CSRGraph = ctx.graph
+        slope, dp, seed, has_bias = ctx.meta
+        dev = x.device
+        g = grad_out.contiguous().to(torch.float32)
+        N, F = x.shape
+        H, C = SUPPORTED_HEADS, weight.size(0) // SUPPORTED_HEADS
+        csc = graph.csc()
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gw = torch.empty_like(weight)
+        gas = torch.empty_like(att_src)
+        gad = torch.empty_like(att_dst)
+        gb = torch.empty((C,), dtype=torch.float32, device=dev) if has_bias else None
+        lib = _lib.load()
+        ws = _ws(lib.gfd_gat_bwd_workspace_size(N, graph.num_messages, F, H, C), dev)
+        _lib.call("gfd_gat_bwd", x.data_ptr(), N, F, F, graph.rowptr.data_ptr(),
+                  graph.col.data_ptr(), csc.colptr.data_ptr(), csc.dst.data_ptr(),
+                  csc.eid.data_ptr(), graph.num_messages, weight.data_ptr(), att_src.data_ptr(),
+                  att_dst.data_ptr(), H, C, slope, dp, seed & (2 ** 64 - 1), st.data_ptr(),
+                  stats.data_ptr(), g.data_ptr(), _lib.ptr(gx), gw.data_ptr(), gas.data_ptr(),
+                  gad.data_ptr(), _lib.ptr(gb), ws.data_ptr(), ws.numel(),
+                  _lib.stream_handle(dev))
+        return gx, gw, gas, gad, gb, None, None, None, None
+
+
+def gat_conv(x: torch.Tensor, edge_index_or_graph, weight: torch.Tensor, att_src: torch.Tensor,
+             att_dst: torch.Tensor, bias: Optional[torch.Tensor], negative_slope: float = 0.2,
+             dropout: float = 0.0, training: bool = False) -> torch.Tensor:
+    """Functional GATConv (heads=8, C=64, concat=False, self loops added)."""
+    graph = edge_index_or_graph
+    if not isinstance(graph, CSRGraph):
+        graph = get_graph(edge_index_or_graph, x.size(0))
+    if graph.num_nodes != x.size(0):
+        raise ValueError(f"graph has {graph.num_nodes} nodes but x has {x.size(0)} rows")
+    dp = float(dropout) if training else 0.0
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if dp > 0 else 0
+    return GATConvFunction.apply(x, weight, att_src.reshape(-1), att_dst.reshape(-1), bias,
+                                 graph, negative_slope, dp, seed)
+
+
+def _glorot(t: torch.Tensor):
+    a = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))
+    with torch.no_grad():
+        t.uniform_(-a, a)
+
+
+class GATConv(nn.Module):
+    """PyG-compatible ``GATConv`` for the reference's configuration.
+
+    Supported: ``heads=8``, ``out_channels=64``, ``concat=False``,
+    ``add_self_loops=True``, any ``in_channels <= 256``, optional bias.
+    Anything else raises ``NotImplementedError`` rather than computing
+    something different from PyG.
+    """
+
+    def __init__(self, in_channels: int, out_channels: int, heads: int = 1, concat: bool = True,
+                 negative_slope: float = 0.2, dropout: float = 0.0, add_self_loops: bool = True,
+                 edge_dim: Optional[int] = None, fill_value="mean", bias: bool = True, **kwargs):
+        super().__init__()
+        if heads != SUPPORTED_HEADS or out_channels != SUPPORTED_CHANNELS or concat:
+            raise NotImplementedError(
+                "gfd GATConv implements the reference's configuration: heads=8, out_channels=64, "
+                f"concat=False (got heads={heads}, out_channels={out_channels}, concat={concat})")
+        if not add_self_loops or edge_dim is not None:
+            raise NotImplementedError("gfd GATConv: add_self_loops=True and no edge features only")
+        if not isinstance(in_channels, int) or not 1 <= in_channels <= 256:
+            raise NotImplementedError("gfd GATConv: int in_channels in [1, 256]")
+        self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
+        self.concat, self.negative_slope, self.dropout = concat, negative_slope, dropout
+        self.add_self_loops = add_self_loops
+        self.lin_src = nn.Linear(in_channels, heads * out_channels, bias=False)
+        self.lin_dst = self.lin_src          # PyG aliases them for int in_channels
+        self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        _glorot(self.lin_src.weight)
+        _glorot(self.att_src)
+        _glorot(self.att_dst)
+        if self.bias is not None:
+            nn.init.zeros_(self.bias)
+
+    def forward(self, x: torch.Tensor, edge_index, size=None, return_attention_weights=None):
+        if return_attention_weights:
+            raise NotImplementedError("gfd GATConv: return_attention_weights is not supported")
+        return gat_conv(x, edge_index, self.lin_src.weight, self.att_src, self.att_dst, self.bias,
+                        self.negative_slope, self.dropout, self.training)
+
+    def extra_repr(self) -> str:
+        return (f"{self.in_channels}, {self.out_channels}, heads={self.heads}, concat=False, "
+                f"dropout={self.dropout}")

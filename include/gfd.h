@@ -1,0 +1,180 @@
+/*
+ * gfd.h -- C ABI of the MI355X-native GATConv engine (libgfd.so, gfx950).
+ *
+ * This is the drop-in boundary for the reference's hot path: the
+ * ``torch_geometric.nn.GATConv`` operator that the reference imports at
+ * /root/reference/src/models/gat.py:4 and tgn.py:4, constructs as
+ * ``GATConv(in, 64, heads=8, concat=False, dropout=p)`` (gat.py:39,45,51;
+ * tgn.py:43,49,55) and calls as ``gat(h, edge_index)`` (gat.py:80, tgn.py:94).
+ * PyG's GATConv is third-party (setup.py:13, unpinned); the interface each entry
+ * point replaces is named next to it.  Plain pointers and sizes only: no torch
+ * types, no HIP headers (a stream is passed as an opaque ``hipStream_t``
+ * handle), so ctypes / cgo / JNI bind it as-is.
+ *
+ * Conventions
+ *  - Every pointer except the ``ws`` workspace and explicitly host-side
+ *    arguments is a DEVICE pointer on the current HIP device.
+ *  - The caller owns all memory, including workspaces; the library allocates
+ *    nothing and keeps no global state.  All work is enqueued on ``stream``;
+ *    nothing synchronises except where a function says so.
+ *  - Floating point is IEEE fp32 at the boundary.  Internally the feature
+ *    projection runs on bf16 MFMA with a 3-term hi/lo split (fp32-faithful to
+ *    ~1e-6 relative); softmax, aggregation and accumulation are fp32.
+ *  - Graph layout: ``edge_index`` is the reference's COO ``int64 [2, E]``
+ *    (dataset.py:104; row 0 = source j, row 1 = destination i, flow
+ *    source->target).  Internally a destination-sorted CSR of int32 with the
+ *    PyG self-loop policy (existing self loops removed, one appended per node,
+ *    duplicates kept): ``rowptr[N+1]``, ``col[E']``, E' = E - loops + N.
+ */
+#ifndef GFD_H
+#define GFD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* gfd_stream_t; /* a hipStream_t; NULL = the null stream */
+typedef int32_t gfd_status;
+
+#define GFD_OK 0
+#define GFD_ERR_ARGUMENT 1    /* null pointer, bad shape, size out of range  (PyG/ATen: ValueError)   */
+#define GFD_ERR_INDEX 2       /* an edge index outside [0, N)                (ATen: index out of range) */
+#define GFD_ERR_WORKSPACE 3   /* ws_bytes smaller than the *_workspace_size answer                     */
+#define GFD_ERR_HIP 4         /* a HIP runtime call or kernel launch failed                            */
+#define GFD_ERR_UNSUPPORTED 5 /* heads/channels/features outside the compiled set (H=8, C=64, F<=256)  */
+
+const char* gfd_status_string(gfd_status status);
+int gfd_abi_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Graph formats.  Replaces PyG's per-call remove_self_loops + add_self_loops
+ * (inside GATConv.forward) and the COO gather/scatter index math.
+ * ------------------------------------------------------------------------- */
+
+/* Workspace for gfd_csr_from_coo (device bytes). */
+size_t gfd_csr_workspace_size(int64_t num_edges, int64_t num_nodes);
+
+/* COO [2,E] int64 -> destination-sorted CSR.  ``col`` must hold E + N entries;
+ * on return rowptr[N] = E'.  Within a destination the original edge order is
+ * kept (stable), and the self loop is last -- PyG's message order.
+ * Validates every index; synchronises ``stream`` once to report
+ * GFD_ERR_INDEX.  Not for the timed path: build once per graph and cache. */
+gfd_status gfd_csr_from_coo(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                            int32_t* rowptr, int32_t* col, void* ws, size_t ws_bytes,
+                            gfd_stream_t stream);
+
+/* Source-sorted view of a CSR (for the backward scatter to sources):
+ * colptr[N+1]; for the k-th message leaving source j (stable in CSR order),
+ * csc_dst[colptr[j]+k] = its destination and csc_eid[...] = its CSR position. */
+size_t gfd_csc_workspace_size(int64_t num_messages, int64_t num_nodes);
+gfd_status gfd_csc_from_csr(const int32_t* rowptr, const int32_t* col, int64_t num_messages,
+                            int64_t num_nodes, int32_t* colptr, int32_t* csc_dst, int32_t* csc_eid,
+                            void* ws, size_t ws_bytes, gfd_stream_t stream);
+
+/* Hub plan: destinations with more than ``hub_threshold`` messages are split
+ * into chunks of at most ``chunk`` messages processed by separate waves and
+ * merged.  Writes (device) hub_rank[num_dst] (-1 light, else hub index),
+ * hub_chunk[4*max_chunks] ({hub, e_begin, e_end, dst}), hub_chunk_ptr[n_hubs+1],
+ * hub_dst[n_hubs], and the HOST counters *num_hubs, *num_chunks.  Synchronises
+ * the stream once.  ``max_chunks``/``max_hubs`` bound the arrays; if exceeded
+ * it returns GFD_ERR_WORKSPACE with the needed counts in the host counters. */
+size_t gfd_plan_workspace_size(int64_t num_dst);
+gfd_status gfd_plan_hubs(const int32_t* rowptr, int64_t num_dst, int32_t hub_threshold,
+                         int32_t chunk, int32_t* hub_rank, int32_t* hub_chunk,
+                         int32_t* hub_chunk_ptr, int32_t* hub_dst, int64_t max_hubs,
+                         int64_t max_chunks, int64_t* num_hubs, int64_t* num_chunks, void* ws,
+                         size_t ws_bytes, gfd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * GATConv forward (PyG GATConv.forward, concat=False, add_self_loops=True,
+ * bias=True; gat.py:80 / tgn.py:94):
+ *   out[i] = mean_h sum_{j in N(i)} alpha_ijh (W_h x_j) + bias
+ *   alpha_ijh = softmax_j(leaky_relu(s_jh + t_ih, slope))  (eps 1e-16)
+ *   s = (x W^T) . att_src, t = (x W^T) . att_dst  per head.
+ * Computed aggregate-then-project: z_ih = sum_j alpha_ijh x_j (fp32), then
+ * out_i = sum_h W_h z_ih / H on MFMA -- x rows (F wide) are gathered, never
+ * the 512-wide projected rows.
+ * ------------------------------------------------------------------------- */
+
+/* Packed weights (device bytes): folded logit vectors and MFMA fragments. */
+size_t gfd_gat_packed_size(int in_features, int heads, int channels);
+
+/* lin_src.weight [H*C, F] row-major, att_src/att_dst [H*C] (PyG [1,H,C]) -> packed. */
+gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const float* att_dst,
+                                int in_features, int heads, int channels, void* packed,
+                                gfd_stream_t stream);
+
+/* Per-node attention logits st[r, 0:H] = s_r, st[r, H:2H] = t_r for rows
+ * r in [0, num_rows) of x (x may point at any row; x_stride in elements). */
+gfd_status gfd_gat_logits(const float* x, int64_t num_rows, int in_features, int64_t x_stride,
+                          const void* packed, int heads, int channels, float* st,
+                          gfd_stream_t stream);
+
+/* Workspace for gfd_gat_aggregate / gfd_gat_fwd (device bytes). */
+size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int in_features, int heads,
+                                  int channels, int64_t num_hubs, int64_t num_chunks);
+
+/* Fused softmax-aggregate-project for destinations [dst_offset, dst_offset+num_dst)
+ * whose CSR slice is rowptr[0..num_dst] (absolute positions into col), sources
+ * are global rows of x (N rows, "halo resident").  st holds logits for all N
+ * rows.  Hub arrays come from gfd_plan_hubs on the same rowptr (NULL with
+ * num_hubs = 0 when no destination exceeds the threshold).
+ * dropout_p > 0 applies dropout to alpha with a counter-based mask keyed by
+ * (seed, CSR position, head) -- reproducible in the backward.
+ * out [num_dst, C]; stats (nullable) [num_dst, 2H] = per-head softmax max and
+ * denominator (sum of exp, without the eps), saved for the backward.
+ * ``stages`` selects GFD_STAGE_HUBS (chunk partials + merge into ws),
+ * GFD_STAGE_TILES (the fused tile kernel, reading merged hub rows from ws) or
+ * GFD_STAGE_ALL; split calls must pass the same ws. */
+#define GFD_STAGE_HUBS 1
+#define GFD_STAGE_TILES 2
+#define GFD_STAGE_ALL 3
+gfd_status gfd_gat_aggregate(const float* x, int64_t num_nodes, int in_features, int64_t x_stride,
+                             const int32_t* rowptr, const int32_t* col, int64_t num_dst,
+                             int64_t dst_offset, const float* st, const void* packed,
+                             const float* bias, int heads, int channels, float negative_slope,
+                             float dropout_p, uint64_t dropout_seed, const int32_t* hub_rank,
+                             const int32_t* hub_chunk, const int32_t* hub_chunk_ptr,
+                             const int32_t* hub_dst, int64_t num_hubs, int64_t num_chunks,
+                             int stages, float* out, float* stats, void* ws, size_t ws_bytes,
+                             gfd_stream_t stream);
+
+/* One-call GATConv forward over the whole graph (num_dst = N, offset 0):
+ * pack weights + logits + aggregate.  ws must hold
+ * gfd_gat_fwd_workspace_size(N, N, F, H, C, num_hubs, num_chunks). */
+gfd_status gfd_gat_fwd(const float* x, int64_t num_nodes, int in_features, int64_t x_stride,
+                       const int32_t* rowptr, const int32_t* col, const float* weight,
+                       const float* att_src, const float* att_dst, const float* bias, int heads,
+                       int channels, float negative_slope, float dropout_p, uint64_t dropout_seed,
+                       const int32_t* hub_rank, const int32_t* hub_chunk,
+                       const int32_t* hub_chunk_ptr, const int32_t* hub_dst, int64_t num_hubs,
+                       int64_t num_chunks, float* out, float* st, float* stats, void* ws,
+                       size_t ws_bytes, gfd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * GATConv backward (autograd of the PyG dataflow).
+ * Given grad_out [N, C], the forward's st [N, 2H] and stats [N, 2H], writes
+ * grad_x [N, F] (nullable), grad_weight [H*C, F], grad_att_src/grad_att_dst
+ * [H*C], grad_bias [C] (nullable).  All outputs are overwritten (not
+ * accumulated).  Needs the CSR and its CSC view.
+ * ------------------------------------------------------------------------- */
+size_t gfd_gat_bwd_workspace_size(int64_t num_nodes, int64_t num_messages, int in_features,
+                                  int heads, int channels);
+
+gfd_status gfd_gat_bwd(const float* x, int64_t num_nodes, int in_features, int64_t x_stride,
+                       const int32_t* rowptr, const int32_t* col, const int32_t* colptr,
+                       const int32_t* csc_dst, const int32_t* csc_eid, int64_t num_messages,
+                       const float* weight, const float* att_src, const float* att_dst,
+                       int heads, int channels, float negative_slope, float dropout_p,
+                       uint64_t dropout_seed, const float* st, const float* stats,
+                       const float* grad_out, float* grad_x, float* grad_weight,
+                       float* grad_att_src, float* grad_att_dst, float* grad_bias, void* ws,
+                       size_t ws_bytes, gfd_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GFD_H */

@@ -1,0 +1,86 @@
+"""CPU: the C-ABI library loads, exports every symbol include/gfd.h declares,
+the ctypes table mirrors the header, and the host-side size/argument logic
+behaves (no kernel is launched: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "gfd.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gfd_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gfd import build, _lib
+    build.build(verbose=False)
+    return _lib.load()
+
+
+def test_header_declares_expected_entry_points():
+    names = _declared()
+    for must in ["gfd_csr_from_coo", "gfd_csc_from_csr", "gfd_plan_hubs", "gfd_gat_fwd",
+                 "gfd_gat_bwd", "gfd_gat_aggregate", "gfd_gat_logits", "gfd_gat_pack_weights"]:
+        assert must in names
+
+
+def test_every_declared_symbol_is_exported(lib):
+    for name in _declared():
+        assert hasattr(lib, name), f"{name} declared in gfd.h but not exported"
+
+
+def test_ctypes_table_matches_header(lib):
+    from gfd import _lib
+    assert sorted(_lib.SIGNATURES) == _declared()
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for name, (_, args) in _lib.SIGNATURES.items():
+        m = re.search(name + r"\s*\(([^;]*)\)\s*;", src)
+        assert m, name
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), f"{name}: header has {len(params)} params, ctypes {len(args)}"
+
+
+def test_version_and_status_strings(lib):
+    assert lib.gfd_abi_version() == 1
+    assert b"range" in lib.gfd_status_string(2)
+    assert lib.gfd_status_string(99) == b"unknown status"
+
+
+def test_workspace_queries(lib):
+    assert lib.gfd_gat_packed_size(166, 8, 64) > 0
+    assert lib.gfd_gat_packed_size(166, 4, 64) == 0          # unsupported heads
+    assert lib.gfd_gat_packed_size(257, 8, 64) == 0          # F > 256
+    small = lib.gfd_gat_fwd_workspace_size(1000, 1000, 166, 8, 64, 0, 0)
+    big = lib.gfd_gat_fwd_workspace_size(1000, 1000, 166, 8, 64, 10, 100)
+    assert big > small > 0
+    assert lib.gfd_csr_workspace_size(10_000, 1000) >= 4 * 4 * 10_000
+    assert lib.gfd_gat_bwd_workspace_size(1000, 5000, 166, 8, 64) >= 2 * 1000 * 512 * 4
+
+
+def test_argument_errors_without_launch(lib):
+    # null pointers / bad shapes are rejected before anything touches a device
+    assert lib.gfd_csr_from_coo(None, 10, 0, None, None, None, 0, None) == 1
+    assert lib.gfd_gat_fwd(None, 10, 166, 166, None, None, None, None, None, None, 8, 64,
+                           ctypes.c_float(0.2), ctypes.c_float(0.0), 0, None, None, None, None,
+                           0, 0, None, None, None, None, 0, None) == 1
+    assert lib.gfd_gat_fwd(None, 10, 166, 166, None, None, None, None, None, None, 4, 64,
+                           ctypes.c_float(0.2), ctypes.c_float(0.0), 0, None, None, None, None,
+                           0, 0, None, None, None, None, 0, None) == 5
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from gfd import _lib
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        saved = _lib._LIB
+        _lib._LIB = None
+        try:
+            _lib.load(str(tmp_path / "nope.so"))
+        finally:
+            _lib._LIB = saved

@@ -1,0 +1,253 @@
+"""GPU parity tests for the GATConv hot path (libgfd.so via the C ABI).
+
+Oracle: oracle/gatconv_ref.py (PyG 2.x GATConv dataflow restated on the CPU),
+pinned by tests/golden/*.npz which were produced by the reference's own model
+code (tests/golden/make_golden.py).  Tolerance: 1e-4 (BASELINE.json north_star).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _util import FWD_ATOL, assert_close, assert_close_scaled, csr_cpu
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _gfd():
+    import gfd.graph as graph
+    import gfd.nn as gnn
+    return gnn, graph
+
+
+def _run_case(arr, name, backward=True):
+    gnn, _ = _gfd()
+    x = torch.from_numpy(arr[f"{name}.x"]).to(DEV).requires_grad_(backward)
+    ei = torch.from_numpy(arr[f"{name}.edge_index"]).to(DEV)
+    W = torch.from_numpy(arr[f"{name}.weight"]).to(DEV).requires_grad_(backward)
+    a_s = torch.from_numpy(arr[f"{name}.att_src"]).to(DEV).requires_grad_(backward)
+    a_d = torch.from_numpy(arr[f"{name}.att_dst"]).to(DEV).requires_grad_(backward)
+    b = torch.from_numpy(arr[f"{name}.bias"]).to(DEV).requires_grad_(backward)
+    out = gnn.gat_conv(x, ei, W, a_s, a_d, b)
+    grads = None
+    if backward:
+        g = torch.from_numpy(arr[f"{name}.grad_out"]).to(DEV)
+        (out * g).sum().backward()
+        grads = {"x": x.grad, "weight": W.grad, "att_src": a_s.grad, "att_dst": a_d.grad,
+                 "bias": b.grad}
+    torch.cuda.synchronize()
+    return out, grads
+
+
+@pytest.mark.parametrize("case", ["base", "scale100"])
+def test_edgecases_forward(golden, case):
+    arr = golden("gatconv_edgecases.npz")
+    out, _ = _run_case(arr, case, backward=False)
+    assert_close(out, arr[f"{case}.out"], what=f"edgecases/{case} out")
+
+
+@pytest.mark.parametrize("case", ["base", "scale100"])
+def test_edgecases_backward(golden, case):
+    arr = golden("gatconv_edgecases.npz")
+    _, grads = _run_case(arr, case)
+    for k, v in grads.items():
+        assert_close_scaled(v.reshape(arr[f"{case}.grad_{k}"].shape), arr[f"{case}.grad_{k}"],
+                            what=f"edgecases/{case} grad_{k}")
+
+
+def test_powerlaw_f166_forward_backward(golden):
+    arr = golden("gatconv_f166.npz")
+    out, grads = _run_case(arr, "pl")
+    assert_close(out, arr["pl.out"], what="f166 out")
+    for k, v in grads.items():
+        assert_close_scaled(v.reshape(arr[f"pl.grad_{k}"].shape), arr[f"pl.grad_{k}"],
+                            what=f"f166 grad_{k}")
+
+
+def _random_case(N, E, F, seed, kind="powerlaw"):
+    from gfd import synth
+    from oracle import GATConvRef
+    if kind == "powerlaw":
+        ei = torch.from_numpy(synth.power_law(N, E, seed=seed))
+        x = torch.randn(N, F, generator=torch.Generator().manual_seed(seed))
+    else:
+        g = synth.elliptic_like(N, E, num_steps=7, num_features=F, seed=seed)
+        ei, x = torch.from_numpy(g["edge_index"]), torch.from_numpy(g["x"])
+    gen = torch.Generator().manual_seed(seed + 1)
+    conv = GATConvRef(F, 64, heads=8, concat=False)
+    conv.reset_parameters(gen)
+    with torch.no_grad():
+        conv.bias.copy_(torch.randn(64, generator=gen))
+    return x, ei, conv
+
+
+@pytest.mark.parametrize("N,E,F,kind", [
+    (1, 0, 166, "powerlaw"),        # single node, no edges (self loop only)
+    (37, 100, 1, "powerlaw"),       # F = 1
+    (300, 2000, 17, "powerlaw"),
+    (1000, 5000, 64, "powerlaw"),   # hidden-layer width
+    (2000, 2300, 165, "elliptic"),  # checkpoint width
+    (2000, 8000, 166, "powerlaw"),  # BASELINE width
+    (500, 3000, 200, "powerlaw"),
+    (333, 4000, 256, "powerlaw"),   # max width
+])
+def test_forward_vs_oracle(N, E, F, kind):
+    gnn, _ = _gfd()
+    x, ei, conv = _random_case(N, E, F, seed=N + F, kind=kind)
+    with torch.no_grad():
+        ref = conv(x, ei)
+        out = gnn.gat_conv(x.to(DEV), ei.to(DEV), conv.lin_src.weight.to(DEV),
+                           conv.att_src.to(DEV), conv.att_dst.to(DEV), conv.bias.to(DEV))
+    assert_close(out, ref, what=f"N={N} E={E} F={F}")
+
+
+def test_backward_vs_oracle_elliptic_like():
+    gnn, _ = _gfd()
+    x, ei, conv = _random_case(3000, 3500, 165, seed=9, kind="elliptic")
+    g = torch.randn(3000, 64, generator=torch.Generator().manual_seed(3))
+    xr = x.clone().requires_grad_(True)
+    (conv(xr, ei) * g).sum().backward()
+    xd = x.to(DEV).requires_grad_(True)
+    W = conv.lin_src.weight.detach().to(DEV).requires_grad_(True)
+    a_s = conv.att_src.detach().to(DEV).requires_grad_(True)
+    a_d = conv.att_dst.detach().to(DEV).requires_grad_(True)
+    b = conv.bias.detach().to(DEV).requires_grad_(True)
+    (gnn.gat_conv(xd, ei.to(DEV), W, a_s, a_d, b) * g.to(DEV)).sum().backward()
+    assert_close_scaled(xd.grad, xr.grad, what="grad_x")
+    assert_close_scaled(W.grad, conv.lin_src.weight.grad, what="grad_W")
+    assert_close_scaled(a_s.grad, conv.att_src.grad, what="grad_att_src")
+    assert_close_scaled(a_d.grad, conv.att_dst.grad, what="grad_att_dst")
+    assert_close_scaled(b.grad, conv.bias.grad, what="grad_bias")
+
+
+@pytest.mark.parametrize("threshold,chunk", [(1, 1), (4, 3), (16, 16), (1 << 30, 128)])
+def test_hub_split_equivalence(threshold, chunk):
+    """Same outputs whatever the hub threshold/chunking (merge is exact math)."""
+    gnn, graph = _gfd()
+    x, ei, conv = _random_case(800, 6000, 166, seed=4)
+    xd, eid = x.to(DEV), ei.to(DEV)
+    g = graph.csr_from_coo(eid, 800)
+    g._hubs = graph.plan_hubs(g.rowptr, g.num_messages, threshold=threshold, chunk=chunk)
+    with torch.no_grad():
+        out = gnn.gat_conv(xd, g, conv.lin_src.weight.to(DEV), conv.att_src.to(DEV),
+                           conv.att_dst.to(DEV), conv.bias.to(DEV))
+        ref = conv(x, ei)
+    assert_close(out, ref, what=f"hub thr={threshold} chunk={chunk}")
+
+
+def test_csr_matches_pyg_self_loop_policy():
+    _, graph = _gfd()
+    rng = np.random.default_rng(0)
+    N = 500
+    ei = rng.integers(0, N, (2, 4000))
+    ei[:, :50] = ei[0, :50]  # self loops in the input
+    ei = torch.from_numpy(ei)
+    g = graph.csr_from_coo(ei.to(DEV), N)
+    rp, col = csr_cpu(ei, N)
+    assert torch.equal(g.rowptr.cpu().long(), rp)
+    assert torch.equal(g.col.cpu().long(), col)          # stable order, loops last
+    csc = g.csc()
+    # every message appears once in the CSC, grouped by source, CSR order inside
+    eid = csc.eid.cpu().long()
+    assert torch.equal(torch.sort(eid).values, torch.arange(g.num_messages))
+    src_sorted = col[eid]
+    assert bool((src_sorted[1:] >= src_sorted[:-1]).all())
+    dst_of = torch.repeat_interleave(torch.arange(N), rp[1:] - rp[:-1])
+    assert torch.equal(csc.dst.cpu().long(), dst_of[eid])
+
+
+def test_index_out_of_range_raises():
+    _, graph = _gfd()
+    ei = torch.tensor([[0, 1, 5], [1, 2, 0]], device=DEV)
+    with pytest.raises(IndexError):
+        graph.csr_from_coo(ei, 5)
+
+
+def test_deterministic_forward():
+    gnn, _ = _gfd()
+    x, ei, conv = _random_case(4000, 30000, 166, seed=2)
+    args = (x.to(DEV), ei.to(DEV), conv.lin_src.weight.to(DEV), conv.att_src.to(DEV),
+            conv.att_dst.to(DEV), conv.bias.to(DEV))
+    with torch.no_grad():
+        a = gnn.gat_conv(*args)
+        b = gnn.gat_conv(*args)
+    assert torch.equal(a, b)
+
+
+def test_dropout_is_reproducible_and_unbiased():
+    """Train-mode dropout on alpha: same seed -> same output; E[out] ~ eval output."""
+    gnn, _ = _gfd()
+    from gfd.nn import GATConvFunction
+    x, ei, conv = _random_case(2000, 20000, 64, seed=5)
+    xd = x.to(DEV)
+    g = _gfd()[1].get_graph(ei.to(DEV), 2000)
+    W, a_s, a_d, b = (conv.lin_src.weight.to(DEV), conv.att_src.to(DEV).reshape(-1),
+                      conv.att_dst.to(DEV).reshape(-1), conv.bias.to(DEV))
+    with torch.no_grad():
+        o1 = GATConvFunction.apply(xd, W, a_s, a_d, b, g, 0.2, 0.2, 1234)
+        o2 = GATConvFunction.apply(xd, W, a_s, a_d, b, g, 0.2, 0.2, 1234)
+        o3 = GATConvFunction.apply(xd, W, a_s, a_d, b, g, 0.2, 0.2, 99)
+        ev = GATConvFunction.apply(xd, W, a_s, a_d, b, g, 0.2, 0.0, 0)
+        avg = sum(GATConvFunction.apply(xd, W, a_s, a_d, b, g, 0.2, 0.2, s) for s in range(64)) / 64
+    assert torch.equal(o1, o2)
+    assert not torch.equal(o1, o3)
+    # unbiased: the mean over seeds approaches the eval output
+    assert (avg - ev).abs().mean() < 0.25 * (o1 - ev).abs().mean()
+
+
+def test_dropout_backward_matches_finite_difference():
+    """Gradient of the dropout path (mask regenerated in the backward)."""
+    from gfd.nn import GATConvFunction
+    _, graph = _gfd()
+    x, ei, conv = _random_case(200, 1500, 32, seed=8)
+    g = graph.get_graph(ei.to(DEV), 200)
+    xd = x.to(DEV).double().float()
+    W = conv.lin_src.weight.detach().to(DEV).requires_grad_(True)
+    a_s = conv.att_src.detach().to(DEV).reshape(-1)
+    a_d = conv.att_dst.detach().to(DEV).reshape(-1)
+    b = conv.bias.detach().to(DEV)
+    go = torch.randn(200, 64, device=DEV)
+    out = GATConvFunction.apply(xd, W, a_s, a_d, b, g, 0.2, 0.3, 77)
+    (out * go).sum().backward()
+    # directional derivative along a random direction
+    d = torch.randn_like(W) * 1e-2
+    with torch.no_grad():
+        fp = (GATConvFunction.apply(xd, W + d, a_s, a_d, b, g, 0.2, 0.3, 77) * go).sum()
+        fm = (GATConvFunction.apply(xd, W - d, a_s, a_d, b, g, 0.2, 0.3, 77) * go).sum()
+    fd = (fp - fm) / 2
+    an = (W.grad * d).sum()
+    assert abs(float(fd - an)) <= 2e-3 * max(1.0, abs(float(an)))
+
+
+@pytest.mark.slow
+def test_full_size_sampled_parity_and_invariants():
+    """C4-shaped graph (2M nodes / 10M edges here to bound test time): exact
+    oracle on a sample of destinations (incl. the biggest hubs) + invariants."""
+    gnn, graph = _gfd()
+    from gfd import synth
+    from oracle import GATConvRef, gatconv_forward_at
+    N, E, F = 2_000_000, 10_000_000, 166
+    ei = synth.power_law_device(N, E, seed=1, device=DEV)
+    x = torch.randn(N, F, device=DEV, generator=torch.Generator(device=DEV).manual_seed(0))
+    conv = GATConvRef(F, 64, heads=8, concat=False)
+    conv.reset_parameters(torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        conv.bias.normal_()
+    g = graph.get_graph(ei, N)
+    assert g.hubs().num_hubs > 0
+    with torch.no_grad():
+        out = gnn.gat_conv(x, g, conv.lin_src.weight.to(DEV), conv.att_src.to(DEV),
+                           conv.att_dst.to(DEV), conv.bias.to(DEV))
+    assert torch.isfinite(out).all()
+    deg = (g.rowptr[1:] - g.rowptr[:-1]).cpu()
+    top = torch.topk(deg, 8).indices
+    rnd = torch.randint(0, N, (256,), generator=torch.Generator().manual_seed(1))
+    dsts = torch.unique(torch.cat([top, rnd]))
+    ref = gatconv_forward_at(x.cpu(), g.rowptr.cpu().long(), g.col.cpu().long(), dsts,
+                             conv.lin_src.weight, conv.att_src, conv.att_dst, conv.bias)
+    assert_close(out[dsts.to(DEV)], ref, what="sampled full-size")
+    # self-loop-only destinations: output is exactly mean_h W_h x_i + b
+    lone = torch.nonzero(deg == 1).flatten()[:64]
+    Wbar = conv.lin_src.weight.view(8, 64, F).mean(0)
+    ref_lone = x.cpu()[lone] @ Wbar.t() + conv.bias
+    assert_close(out[lone.to(DEV)], ref_lone.detach(), what="self-loop-only rows")
