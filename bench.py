@@ -134,7 +134,9 @@ def main():
     del ei
     torch.cuda.empty_cache()
     gx = torch.Generator(device=dev).manual_seed(0)
-    x = torch.randn((N, F), generator=gx, device=dev, dtype=torch.float32)
+    LDX = (F + 3) // 4 * 4  # row pitch 168 for F = 166 (16-B aligned rows)
+    xbuf = torch.randn((N, LDX), generator=gx, device=dev, dtype=torch.float32)
+    x = xbuf[:, :F]
     gen = torch.Generator().manual_seed(0)
     W = glorot((H * C, F), gen, dev).contiguous()
     a_s = glorot((1, H, C), gen, dev).contiguous()
@@ -143,7 +145,7 @@ def main():
 
     lo, hi = gdist.shard_ranges(g.rowptr, rank, world) if world > 1 else (0, N)
     shard = g.shard(lo, hi)
-    hubs = shard.hubs
+    plan = shard.plan
     n_dst = hi - lo
     m_local = int(shard.rowptr[-1].item()) - int(shard.rowptr[0].item())
     nb = gdist.node_bounds(N, world)
@@ -153,28 +155,28 @@ def main():
     st = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
     st_local = torch.empty((max(st_hi - st_lo, 1), 2 * H), dtype=torch.float32, device=dev)
     out = torch.empty((max(n_dst, 1), C), dtype=torch.float32, device=dev)
-    ws = torch.empty(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, hubs.num_hubs,
-                                                    hubs.num_chunks), dtype=torch.uint8, device=dev)
+    ws = torch.empty(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, plan.num_hubs,
+                                                    plan.num_chunks), dtype=torch.uint8, device=dev)
     stream = _lib.stream_handle(dev)
-    hub_args = hubs.args()
+    cplan = plan.cstruct()
 
     def pack_and_logits():
         _lib.call("gfd_gat_pack_weights", W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), F, H, C,
                   packed.data_ptr(), stream)
         if world == 1:
-            _lib.call("gfd_gat_logits", x.data_ptr(), N, F, F, packed.data_ptr(), H, C,
+            _lib.call("gfd_gat_logits", x.data_ptr(), N, F, LDX, packed.data_ptr(), H, C,
                       st.data_ptr(), stream)
         else:
             rows = st_hi - st_lo
             if rows > 0:
-                _lib.call("gfd_gat_logits", x[st_lo:].data_ptr(), rows, F, F, packed.data_ptr(),
+                _lib.call("gfd_gat_logits", x[st_lo:].data_ptr(), rows, F, LDX, packed.data_ptr(),
                           H, C, st_local.data_ptr(), stream)
             st.copy_(gdist.all_gather_rows(st_local[:rows], N, world))
 
     def aggregate(stage):
-        _lib.call("gfd_gat_aggregate", x.data_ptr(), N, F, F, shard.rowptr.data_ptr(),
+        _lib.call("gfd_gat_aggregate", x.data_ptr(), N, F, LDX, shard.rowptr.data_ptr(),
                   g.col.data_ptr(), n_dst, lo, st.data_ptr(), packed.data_ptr(),
-                  bias.data_ptr(), H, C, 0.2, 0.0, 0, *hub_args, stage, out.data_ptr(), None,
+                  bias.data_ptr(), H, C, 0.2, 0.0, 0, cplan, stage, out.data_ptr(), None,
                   ws.data_ptr(), ws.numel(), stream)
 
     def step(evs=None):
@@ -191,7 +193,7 @@ def main():
             evs[3].record()
 
     log(f"[bench] rank {rank}/{world}: N={N} E={E} messages={g.num_messages} shard=[{lo},{hi}) "
-        f"local msgs={m_local} hubs={hubs.num_hubs} chunks={hubs.num_chunks} "
+        f"local msgs={m_local} hubs={plan.num_hubs} chunks={plan.num_chunks} "
         f"setup {time.perf_counter() - t_setup:.1f}s")
     for _ in range(args.warmup):
         step()
@@ -227,10 +229,7 @@ def main():
     flop_layer = 2 * N * F * H * C + M * H * (2 * C + 8)
     t_roof = max(B_layer / (HBM_PEAK_GBPS * 1e9), flop_layer / (BF16_PEAK_TFLOPS * 1e12))
     # dominant kernel = k_fused (tile stage) on this rank: the light messages + all its rows
-    hub_msgs = 0
-    if hubs.num_hubs > 0:
-        ck = hubs.hub_chunk.view(-1, 4).cpu()
-        hub_msgs = int((ck[:, 2] - ck[:, 1]).sum())
+    hub_msgs = plan.hub_messages()
     light_msgs = m_local - hub_msgs
     B_tile = light_msgs * (s * F + 4) + n_dst * (4 + 4 * C) + 4 * F * H * C
     t_tile = sorted(tile_ms)[len(tile_ms) // 2] * 1e-3
@@ -249,7 +248,7 @@ def main():
         "config": {"workload": workload, "nodes": N, "input_edges": E, "messages": M,
                    "features": F, "heads": H, "channels": C,
                    "parallelism": f"dst-shard x{world}" if world > 1 else "single GPU",
-                   "hubs": hubs.num_hubs, "hub_chunks": hubs.num_chunks},
+                   "hubs": plan.num_hubs, "hub_chunks": plan.num_chunks},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "kernel": "k_fused (tile stage)", "algorithmic_bytes": B_tile,
@@ -263,7 +262,7 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        del x, out, ws, st, g
+        del x, xbuf, out, ws, st, g
         torch.cuda.empty_cache()
         log("[bench] timing CPU baseline (oracle, bounded sample) ...")
         res["cpu_baseline"] = cpu_baseline(args)

@@ -2,18 +2,19 @@
 // called at /root/reference/src/models/gat.py:80 and tgn.py:94).
 //
 // Dataflow (aggregate-then-project; SURVEY.md §7 "hard parts"):
-//   k_pack      W [H*C,F], att -> folded logit vectors U/V [2H][Fp] and the
-//               bf16 hi/lo MFMA B-fragments of Wcat[(h,f)][c] = W[h*C+c][f] / H
-//   k_logits    st[n] = (x_n.U_h, x_n.V_h)            -- one x read, 2H outputs
-//   k_fused     per 16-destination tile:
-//               phase A  per destination: two passes over its CSR segment --
-//                        max of leaky(s_j + t_i), then p = exp(e - max),
-//                        z_ih += p x_j (x rows gathered once, all 8 heads),
-//                        z_ih /= sum p + 1e-16 -> Z tile in LDS (fp32)
-//               phase B  out = Z . Wcat + bias on bf16 MFMA 16x16x32 with
-//                        the 3-term split (Zhi.Whi + Zhi.Wlo + Zlo.Whi)
-//   k_hub_*     destinations with > threshold messages are split into chunks
-//               (partial max/sum/z per chunk) and merged before the tile.
+//   k_wmax/k_pack  W [H*C,F], att -> folded logit vectors U/V [2H][Fu] and the
+//                  fp16 hi/lo MFMA B-fragments of Wcat[(h,f)][c] = W[h*C+c][f]/H
+//                  scaled by a power of two 2^kw (max |W| -> 2^14)
+//   k_logits       st[n] = (x_n.U_h, x_n.V_h) on fp32 MFMA (exact fp32 chains)
+//   k_fused        per 16-destination tile (rows taken in descending-degree order):
+//     phase A      one destination per wave: online softmax over its CSR segment
+//                  (max of leaky(s_j + t_i), p = exp(e - max)), z_ih += p x_j with
+//                  the x row gathered once for all 8 heads, z /= sum p + 1e-16
+//     phase B      out = Z . Wcat + bias on f16 MFMA 16x16x32, two head-halves
+//                  through a 43 KB LDS tile; 3-term split hi.hi + (hi.lo + lo.hi)/2^11
+//                  on power-of-two-scaled rows: ~2^-21 relative, fp32-faithful
+//   k_hub_*        destinations with > threshold messages: chunk partials, per-hub
+//                  (max, sum), merged z rows read by the tile kernel
 #include "gfd_common.h"
 
 using namespace gfd;
@@ -22,34 +23,68 @@ namespace {
 
 constexpr int H = kHeads;
 constexpr int C = kChannels;
-constexpr int kTile = 16;          // destinations per fused block (MFMA M)
-constexpr int kFusedThreads = 512; // 8 waves
+constexpr int kTile = 16;       // destinations per fused block (MFMA M)
+constexpr int kFusedWaves = 16; // one destination per wave
+constexpr float kScaleTarget = 16384.f;  // 2^14: scaled |values| stay inside fp16
+constexpr float kLoScale = 2048.f;        // 2^11: lo parts re-normalised into fp16
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 struct PackLayout {
-  int F, Fp, KP, KS;
-  size_t uv_off, whi_off, wlo_off, bytes;
+  int F, Fp, Fu, KP, KS, KH;
+  size_t hdr_off, uv_off, whi_off, wlo_off, bytes;
 };
 
 inline PackLayout pack_layout(int F) {
   PackLayout L;
   L.F = F;
-  L.Fp = (F + 3) / 4 * 4;
-  L.KP = H * L.Fp;          // multiple of 32
-  L.KS = L.KP / 32;         // MFMA k-steps
+  L.Fp = (F + 7) / 8 * 8;   // K per head; 4*Fp (a head-half) is a multiple of 32
+  L.Fu = (F + 15) / 16 * 16; // logit-vector row stride (vector loads never cross rows)
+  L.KP = H * L.Fp;
+  L.KS = L.KP / 32;          // MFMA k-steps
+  L.KH = L.KS / 2;           // k-steps per head-half
   size_t o = 0;
-  L.uv_off = o; o = align_up(o + sizeof(float) * 2 * H * L.Fp, 256);
+  L.hdr_off = o; o = align_up(o + 64, 256);
+  L.uv_off = o; o = align_up(o + sizeof(float) * 2 * H * L.Fu, 256);
   L.whi_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
   L.wlo_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
   L.bytes = o;
   return L;
 }
 
+struct PackHeader {  // device-side, written by k_wmax
+  float w_unscale;   // 2^-kw
+  float w_scale;     // 2^kw
+};
+
 // ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_wmax(const float* __restrict__ W, int n,
+                                              PackHeader* __restrict__ hdr) {
+  __shared__ float red[256];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(W[i]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float wm = red[0] * (1.0f / H);  // the packed values are W / H
+    int ex = 0;
+    if (wm > 0.f) frexpf(wm, &ex);         // wm < 2^ex
+    int kw = 14 - ex;
+    kw = kw > 100 ? 100 : (kw < -100 ? -100 : kw);
+    hdr->w_scale = ldexpf(1.0f, kw);
+    hdr->w_unscale = ldexpf(1.0f, -kw);
+  }
+}
+
 __global__ void k_pack_uv(const float* __restrict__ W, const float* __restrict__ as,
-                          const float* __restrict__ ad, int F, int Fp, float* __restrict__ uv) {
+                          const float* __restrict__ ad, int F, int Fu, float* __restrict__ uv) {
   int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= 2 * H * Fp) return;
-  int q = idx / Fp, f = idx % Fp;
+  if (idx >= 2 * H * Fu) return;
+  int q = idx / Fu, f = idx % Fu;
   int h = q % H;
   const float* a = (q < H ? as : ad) + h * C;
   float acc = 0.f;
@@ -60,83 +95,91 @@ __global__ void k_pack_uv(const float* __restrict__ W, const float* __restrict__
 }
 
 __global__ void k_pack_frag(const float* __restrict__ W, int F, int Fp, int KS,
-                            uint4* __restrict__ whi, uint4* __restrict__ wlo) {
+                            const PackHeader* __restrict__ hdr, uint4* __restrict__ whi,
+                            uint4* __restrict__ wlo) {
   int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (s, ct, lane)
   if (idx >= KS * 4 * 64) return;
   int lane = idx & 63, ct = (idx >> 6) & 3, s = idx >> 8;
   int n = ct * 16 + (lane & 15);
-  union { uint4 v; uint16_t u[8]; } hi, lo;
+  const float sc = hdr->w_scale * (1.0f / H);
+  union { uint4 v; _Float16 h[8]; } hi, lo;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     int k = 32 * s + 8 * (lane >> 4) + j;
     int h = k / Fp, f = k % Fp;
-    float v = (f < F) ? W[size_t(h * C + n) * F + f] * (1.0f / H) : 0.f;
-    uint16_t hb = bf16_bits(v);
-    hi.u[j] = hb;
-    lo.u[j] = bf16_bits(v - bf16_to_f32(hb));
+    float v = (f < F) ? W[size_t(h * C + n) * F + f] * sc : 0.f;
+    _Float16 hv = (_Float16)v;
+    hi.h[j] = hv;
+    lo.h[j] = (_Float16)((v - (float)hv) * kLoScale);
   }
   whi[idx] = hi.v;
   wlo[idx] = lo.v;
 }
 
 // ---------------------------------------------------------------------------
-// st[r][q] = sum_f x[r][f] * uv[q][f], q < 2H.  One wave per row; the 16 dot
-// products are reduced with a transposing butterfly (17 shuffles per row).
-template <int KF>
+// st[r][q] = sum_f x[r][f] * uv[q][f] (q < 2H) on v_mfma_f32_16x16x4_f32.  A
+// wave computes 16 rows x 16 logits.  Lane group g = l >> 4 reads VEC
+// consecutive features k0 + VEC*g .. of its row l & 15 (one vector load), and
+// MFMA step t pairs them with uv[l & 15][k0 + VEC*g + t]: the k order inside a
+// 4*VEC block is permuted identically on both operands, so the sum is exact
+// fp32 FMA chains over all F features.
+template <int VEC>
 __global__ void __launch_bounds__(256) k_logits(const float* __restrict__ x, int64_t rows, int F,
-                                                int64_t ldx, const float* __restrict__ uv, int Fp,
+                                                int64_t ldx, const float* __restrict__ uv, int Fu,
                                                 float* __restrict__ st) {
-  extern __shared__ __attribute__((aligned(16))) float s_uv[];  // [16][Fp]
-  for (int i = threadIdx.x; i < 2 * H * Fp; i += blockDim.x) s_uv[i] = uv[i];
-  __syncthreads();
   const int lane = threadIdx.x & 63;
+  const int rl = lane & 15, g = lane >> 4;
   const int64_t wave = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   const int64_t nwave = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t r = wave; r < rows; r += nwave) {
-    const float* xr = x + r * ldx;
-    float xv[KF];
-#pragma unroll
-    for (int k = 0; k < KF; ++k) {
-      int f = lane + 64 * k;
-      xv[k] = f < F ? xr[f] : 0.f;
-    }
-    float v[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      float a = 0.f;
-#pragma unroll
-      for (int k = 0; k < KF; ++k) {
-        int f = lane + 64 * k;
-        a = fmaf(xv[k], f < Fp ? s_uv[q * Fp + f] : 0.f, a);
+  const int64_t tiles = (rows + 15) / 16;
+  const float* ub = uv + rl * Fu + VEC * g;
+  const int Ffull = F / (4 * VEC) * (4 * VEC);  // blocks fully inside the row
+  for (int64_t t = wave; t < tiles; t += nwave) {
+    const int64_t row = t * 16 + rl;
+    const float* xr = x + (row < rows ? row : rows - 1) * ldx + VEC * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int k0 = 0;
+#pragma unroll 4
+    for (; k0 < Ffull; k0 += 4 * VEC) {
+      float a[VEC], b[VEC];
+      if constexpr (VEC == 4) {
+        *reinterpret_cast<float4*>(a) = *reinterpret_cast<const float4*>(xr + k0);
+        *reinterpret_cast<float4*>(b) = *reinterpret_cast<const float4*>(ub + k0);
+      } else if constexpr (VEC == 2) {
+        *reinterpret_cast<float2*>(a) = *reinterpret_cast<const float2*>(xr + k0);
+        *reinterpret_cast<float2*>(b) = *reinterpret_cast<const float2*>(ub + k0);
+      } else {
+        a[0] = xr[k0];
+        b[0] = ub[k0];
       }
-      v[q] = a;
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc, 0, 0, 0);
     }
-    // transposing butterfly: after xor 32,16,8,4 lane holds index q = lane>>2
+    for (; k0 < F; k0 += 4 * VEC) {  // ragged tail: guarded scalar loads
 #pragma unroll
-    for (int step = 0; step < 4; ++step) {
-      const int half = 8 >> step;        // 8,4,2,1 values kept
-      const int mask = 32 >> step;       // 32,16,8,4
-      const bool up = (lane & mask) != 0;
-#pragma unroll
-      for (int i = 0; i < half; ++i) {
-        float send = up ? v[i] : v[i + half];
-        float keep = up ? v[i + half] : v[i];
-        v[i] = keep + __shfl_xor(send, mask);
+      for (int u = 0; u < VEC; ++u) {
+        const int f = k0 + VEC * g + u;
+        const float xv = xr[(f < F ? f : F - 1) - VEC * g];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(f < F ? xv : 0.f, ub[k0 + u], acc, 0, 0, 0);
       }
     }
-    float t = v[0];
-    t += __shfl_xor(t, 2);
-    t += __shfl_xor(t, 1);
-    if ((lane & 3) == 0) st[r * 16 + (lane >> 2)] = t;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t orow = t * 16 + 4 * g + r;
+      if (orow < rows) st[orow * 16 + rl] = acc[r];
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
-// Online part shared by the fused tile and the hub chunks.  Lane layout for
-// the logits: lane = 8*k + h (edge k of a batch of 8, head h).
+// One destination segment (or hub chunk) on one wave, single pass with an
+// online softmax.  Logit lane layout: lane = 8*k + h (message k of a batch of
+// 8, head h); aggregation lane layout: lane <-> feature f = lane + 64q.
+// Returns the running max m (head lane & 7) and the denominator reduced over
+// the batch lanes; acc[h][q] = sum_j p_jh x_j[f] relative to m.
 struct SegState {
-  float m;     // max of head (lane & 7), valid in every lane after pass 1
-  float ssum;  // denominator of head (lane & 7), reduced in every lane
+  float m;
+  float ssum;
 };
 
 template <int KF>
@@ -146,147 +189,238 @@ __device__ __forceinline__ SegState aggregate_segment(
     float (&acc)[H][KF]) {
   const int lane = threadIdx.x & 63;
   const int h = lane & 7, kk = lane >> 3;
-  // pass 1: max over the segment
-  float m = -INFINITY;
-  for (int b = e0; b < e1; b += 8) {
-    int e = b + kk;
-    if (e < e1) {
-      int j = col[e];
-      m = fmaxf(m, leaky(st[int64_t(j) * 16 + h] + t_h, slope));
-    }
-  }
-  m = fmaxf(m, __shfl_xor(m, 8));
-  m = fmaxf(m, __shfl_xor(m, 16));
-  m = fmaxf(m, __shfl_xor(m, 32));
-  // pass 2: p = exp(e - max), z += p * x_j
+  const float keep_scale = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
 #pragma unroll
   for (int hh = 0; hh < H; ++hh)
 #pragma unroll
-    for (int k = 0; k < KF; ++k) acc[hh][k] = 0.f;
-  float ssum = 0.f;
-  const float keep_scale = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+    for (int q = 0; q < KF; ++q) acc[hh][q] = 0.f;
+  float m = -INFINITY, l = 0.f;
   for (int b = e0; b < e1; b += 8) {
-    int e = b + kk;
-    int j = 0;
-    float p = 0.f;
-    if (e < e1) {
-      j = col[e];
-      p = __expf(leaky(st[int64_t(j) * 16 + h] + t_h, slope) - m);
-      ssum += p;
-      if (dp > 0.f) p = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? p * keep_scale : 0.f;
+    const int e = b + kk;
+    const bool valid = e < e1;
+    const int j = col[valid ? e : e1 - 1];  // clamped: every load is in bounds
+    const float v = leaky(st[int64_t(j) * 16 + h] + t_h, slope);
+    float bm = valid ? v : -INFINITY;
+    bm = fmaxf(bm, __shfl_xor(bm, 8));
+    bm = fmaxf(bm, __shfl_xor(bm, 16));
+    bm = fmaxf(bm, __shfl_xor(bm, 32));
+    const float mn = fmaxf(m, bm);
+    const float sc = __expf(m - mn);  // 0 on the first batch, 1 while the max holds
+    float p = valid ? __expf(v - mn) : 0.f;
+    l = fmaf(l, sc, p);
+    if (b != e0 && __any(sc != 1.0f)) {  // wave-uniform: rescale the running sums
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
+#pragma unroll
+        for (int q = 0; q < KF; ++q) acc[hh][q] *= s;
+      }
     }
+    m = mn;
+    if (dp > 0.f) p = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? p * keep_scale : 0.f;
     const int nk = min(8, e1 - b);
+    for (int k0 = 0; k0 < nk; k0 += 4) {  // sub-batches of 4 rows, loads issued together
+      float xv[4][KF];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (k < nk) {
-        const int jk = __builtin_amdgcn_readlane(j, 8 * k);
-        float pk[H];
-#pragma unroll
-        for (int hh = 0; hh < H; ++hh)
-          pk[hh] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 8 * k + hh));
+      for (int k = 0; k < 4; ++k) {
+        const int jk = __builtin_amdgcn_readlane(j, 8 * (k0 + k));
         const float* xr = x + int64_t(jk) * ldx;
 #pragma unroll
         for (int q = 0; q < KF; ++q) {
           const int f = lane + 64 * q;
-          const float xv = f < F ? xr[f] : 0.f;
+          const float t = xr[f < F ? f : F - 1];
+          xv[k][q] = f < F ? t : 0.f;
+        }
+      }
 #pragma unroll
-          for (int hh = 0; hh < H; ++hh) acc[hh][q] = fmaf(pk[hh], xv, acc[hh][q]);
+      for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {
+          // p of a padding message is 0: its clamped row adds nothing
+          const float pk =
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 8 * (k0 + k) + hh));
+#pragma unroll
+          for (int q = 0; q < KF; ++q) acc[hh][q] = fmaf(pk, xv[k][q], acc[hh][q]);
         }
       }
     }
   }
-  ssum += __shfl_xor(ssum, 8);
-  ssum += __shfl_xor(ssum, 16);
-  ssum += __shfl_xor(ssum, 32);
-  return {m, ssum};
+  l += __shfl_xor(l, 8);
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  return {m, l};
+}
+
+// split 8 fp32 (|v| <= 2^14) into fp16 hi and lo' = (v - hi) * 2^11
+__device__ __forceinline__ void split8_f16(const float* v, f16x8& hi, f16x8& lo) {
+  union { f16x8 v; _Float16 h[8]; } a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 hv = (_Float16)v[j];
+    a.h[j] = hv;
+    b.h[j] = (_Float16)((v[j] - (float)hv) * kLoScale);
+  }
+  hi = a.v;
+  lo = b.v;
+}
+
+__device__ __forceinline__ void mfma_step(const float* __restrict__ Zrow, const uint4& bh,
+                                          const uint4& bl, f32x4& acc_m, f32x4& acc_x) {
+  float a8[8];
+  *reinterpret_cast<float4*>(a8) = *reinterpret_cast<const float4*>(Zrow);
+  *reinterpret_cast<float4*>(a8 + 4) = *reinterpret_cast<const float4*>(Zrow + 4);
+  f16x8 ahi, alo;
+  split8_f16(a8, ahi, alo);
+  const f16x8 bhi = *reinterpret_cast<const f16x8*>(&bh);
+  const f16x8 blo = *reinterpret_cast<const f16x8*>(&bl);
+  acc_m = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bhi, acc_m, 0, 0, 0);
+  acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc_x, 0, 0, 0);
+  acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bhi, acc_x, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
+// Fused tile kernel: 16 destinations per block, one per wave.  The Z tile goes
+// through LDS one head-half at a time (16 x 4Fp fp32 = 43 KB at F = 166, two
+// blocks per CU).  MFMA work split: column tile ct = w & 3, k-step phase kq = w >> 2;
+// the four k-phase partials are summed through LDS at the end.
 template <int KF>
-__global__ void __launch_bounds__(kFusedThreads) k_fused(
+__global__ void __launch_bounds__(1024, 8) k_fused(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, int64_t num_dst, int64_t dst_offset,
-    const float* __restrict__ st, const uint4* __restrict__ whi, const uint4* __restrict__ wlo,
-    const float* __restrict__ bias, float slope, float dp, uint64_t seed,
-    const int32_t* __restrict__ hub_rank, const float* __restrict__ zhub,
+    const int32_t* __restrict__ order, const float* __restrict__ st,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ whi,
+    const uint4* __restrict__ wlo, const float* __restrict__ bias, float slope, float dp,
+    uint64_t seed, const int32_t* __restrict__ hub_rank, const float* __restrict__ zhub,
     float* __restrict__ out, float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int KP = H * Fp;
-  const int ZS = KP + 4;                  // padded row stride (bank spread)
-  float* Z = smem;                        // [kTile][ZS]
-  float* red = smem + kTile * ZS;         // [4][64][4] partials of the upper K half
+  const int KH4 = 4 * Fp;                 // K of one head-half
+  const int ZS = KH4 + 4;                 // padded row stride
+  const int KH = KH4 / 32;                // k-steps per half
+  float* Z = smem;                        // [16][ZS]
+  float* red = Z + kTile * ZS;            // [3][4][64][4] k-phase partials (x2: main, cross)
+  float* rscale = red + 2 * 3 * 4 * 64 * 4;   // [16] per-row 2^-e
+  int* rowid = reinterpret_cast<int*>(rscale + kTile);  // [16]
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
-  const int64_t tile0 = int64_t(blockIdx.x) * kTile;
+  const int64_t slot = int64_t(blockIdx.x) * kTile + wave;
+  const int ct = wave & 3, kq = wave >> 2;
 
-  // ---- phase A: aggregate two destinations per wave into the Z tile ----
-  for (int rr = 0; rr < 2; ++rr) {
-    const int r = wave * 2 + rr;
-    const int64_t i = tile0 + r;
-    float* zr = Z + r * ZS;
-    if (i >= num_dst) {
-      for (int k = lane; k < KP; k += 64) zr[k] = 0.f;
-      continue;
-    }
+  // ---- phase A: this wave's destination, all heads, in registers ----
+  float z[H][KF];
+  int64_t i = -1;
+  if (slot < num_dst) i = order ? order[slot] : slot;
+  if (i >= 0) {
     const int hr = hub_rank ? hub_rank[i] : -1;
-    if (hr >= 0) {  // merged by k_hub_merge
-      const float* src = zhub + int64_t(hr) * KP;
-      for (int k = lane; k < KP; k += 64) zr[k] = src[k];
-      continue;
-    }
-    const int e0 = rowptr[i], e1 = rowptr[i + 1];
-    const int64_t gi = dst_offset + i;
-    const float t_h = st[gi * 16 + H + (lane & 7)];
-    float acc[H][KF];
-    SegState S = aggregate_segment<KF>(x, ldx, F, col, e0, e1, st, t_h, slope, dp, seed, acc);
-    const float inv_lane = 1.0f / (S.ssum + kSoftmaxEps);
-    if (stats && lane < 8) {
-      stats[i * 16 + lane] = S.m;
-      stats[i * 16 + 8 + lane] = S.ssum;
-    }
+    if (hr >= 0) {  // merged (normalised) by k_hub_merge
+      const float* src = zhub + int64_t(hr) * (H * Fp);
 #pragma unroll
-    for (int hh = 0; hh < H; ++hh) {
-      const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_lane), hh));
+      for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+        for (int q = 0; q < KF; ++q) {
+          const int f = lane + 64 * q;
+          z[hh][q] = f < Fp ? src[hh * Fp + f] : 0.f;
+        }
+    } else {
+      const int e0 = rowptr[i], e1 = rowptr[i + 1];
+      const float t_h = st[(dst_offset + i) * 16 + H + (lane & 7)];
+      SegState S = aggregate_segment<KF>(x, ldx, F, col, e0, e1, st, t_h, slope, dp, seed, z);
+      const float inv_lane = 1.0f / (S.ssum + kSoftmaxEps);
+      if (stats && lane < 8) {
+        stats[i * 16 + lane] = S.m;
+        stats[i * 16 + 8 + lane] = S.ssum;
+      }
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_lane), hh));
+#pragma unroll
+        for (int q = 0; q < KF; ++q) z[hh][q] *= inv;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+      for (int q = 0; q < KF; ++q) z[hh][q] = 0.f;
+  }
+  // power-of-two row scale: max |z| -> [2^13, 2^14)
+  float zm = 0.f;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) zm = fmaxf(zm, fabsf(z[hh][q]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) zm = fmaxf(zm, __shfl_xor(zm, o));
+  int ex = 0;
+  if (zm > 0.f) frexpf(zm, &ex);
+  int er = 14 - ex;
+  er = er > 100 ? 100 : (er < -100 ? -100 : er);
+  const float rs = ldexpf(1.0f, er);
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) z[hh][q] *= rs;
+  if (lane == 0) {
+    rscale[wave] = ldexpf(1.0f, -er);
+    rowid[wave] = int(i);
+  }
+
+  // ---- phase B over two head-halves ----
+  const int arow = lane & 15, akg = lane >> 4;
+  f32x4 acc_m = {0.f, 0.f, 0.f, 0.f}, acc_x = {0.f, 0.f, 0.f, 0.f};
+  float* zr = Z + wave * ZS;
+#pragma unroll
+  for (int hg = 0; hg < 2; ++hg) {
+    // W fragments of this wave's first two k-steps: in flight across the barrier
+    const int gs0 = hg * KH;
+    uint4 bh0 = {0, 0, 0, 0}, bl0 = {0, 0, 0, 0}, bh1 = {0, 0, 0, 0}, bl1 = {0, 0, 0, 0};
+    if (kq < KH) {
+      bh0 = whi[((gs0 + kq) * 4 + ct) * 64 + lane];
+      bl0 = wlo[((gs0 + kq) * 4 + ct) * 64 + lane];
+    }
+    if (kq + 4 < KH) {
+      bh1 = whi[((gs0 + kq + 4) * 4 + ct) * 64 + lane];
+      bl1 = wlo[((gs0 + kq + 4) * 4 + ct) * 64 + lane];
+    }
+    if (hg) __syncthreads();  // half 0 fully consumed
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh)
 #pragma unroll
       for (int q = 0; q < KF; ++q) {
         const int f = lane + 64 * q;
-        if (f < Fp) zr[hh * Fp + f] = acc[hh][q] * inv;
+        if (f < Fp) zr[hh * Fp + f] = z[4 * hg + hh][q];
+      }
+    __syncthreads();
+    const float* zb = Z + arow * ZS + 8 * akg;
+    for (int s = kq; s < KH; s += 8) {
+      mfma_step(zb + 32 * s, bh0, bl0, acc_m, acc_x);
+      if (s + 8 < KH) {
+        bh0 = whi[((gs0 + s + 8) * 4 + ct) * 64 + lane];
+        bl0 = wlo[((gs0 + s + 8) * 4 + ct) * 64 + lane];
+      }
+      if (s + 4 < KH) {
+        mfma_step(zb + 32 * (s + 4), bh1, bl1, acc_m, acc_x);
+        if (s + 12 < KH) {
+          bh1 = whi[((gs0 + s + 12) * 4 + ct) * 64 + lane];
+          bl1 = wlo[((gs0 + s + 12) * 4 + ct) * 64 + lane];
+        }
       }
     }
   }
+  f32x4 accv = acc_m + acc_x * (1.0f / kLoScale);
+  if (kq) *reinterpret_cast<f32x4*>(red + (((kq - 1) * 4 + ct) * 64 + lane) * 4) = accv;
   __syncthreads();
-
-  // ---- phase B: out[16 x 64] = Z[16 x KP] . Wcat[KP x 64] on MFMA ----
-  const int ct = wave & 3, kh = wave >> 2;
-  const int KS = KP / 32;
-  const int s0 = kh ? KS / 2 : 0, s1 = kh ? KS : KS / 2;
-  f32x4 accv = {0.f, 0.f, 0.f, 0.f};
-  const int arow = lane & 15, akg = lane >> 4;
-  for (int s = s0; s < s1; ++s) {
-    const float* zp = Z + arow * ZS + 32 * s + 8 * akg;
-    float a8[8];
-    *reinterpret_cast<float4*>(a8) = *reinterpret_cast<const float4*>(zp);
-    *reinterpret_cast<float4*>(a8 + 4) = *reinterpret_cast<const float4*>(zp + 4);
-    bf16x8 ahi, alo;
-    split8(a8, ahi, alo);
-    const uint4 bh = whi[(s * 4 + ct) * 64 + lane];
-    const uint4 bl = wlo[(s * 4 + ct) * 64 + lane];
-    const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&bh);
-    const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&bl);
-    accv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, accv, 0, 0, 0);
-    accv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, accv, 0, 0, 0);
-    accv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, accv, 0, 0, 0);
-  }
-  if (kh) *reinterpret_cast<f32x4*>(red + (ct * 64 + lane) * 4) = accv;
-  __syncthreads();
-  if (!kh) {
-    accv += *reinterpret_cast<const f32x4*>(red + (ct * 64 + lane) * 4);
+  if (!kq) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      accv += *reinterpret_cast<const f32x4*>(red + ((p * 4 + ct) * 64 + lane) * 4);
     const int n = ct * 16 + (lane & 15);
     const float b = bias ? bias[n] : 0.f;
+    const float wu = hdr->w_unscale;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int64_t i = tile0 + (lane >> 4) * 4 + q;
-      if (i < num_dst) out[i * C + n] = accv[q] + b;
+      const int r = (lane >> 4) * 4 + q;
+      const int ri = rowid[r];
+      if (ri >= 0) out[int64_t(ri) * C + n] = accv[q] * (rscale[r] * wu) + b;
     }
   }
 }
@@ -302,8 +436,7 @@ __global__ void __launch_bounds__(256) k_hub_partial(
   const int64_t c = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   if (c >= num_chunks) return;
   const int4 ck = chunks[c];
-  const int64_t gi = dst_offset + ck.w;
-  const float t_h = st[gi * 16 + H + (lane & 7)];
+  const float t_h = st[(dst_offset + ck.w) * 16 + H + (lane & 7)];
   float acc[H][KF];
   SegState S = aggregate_segment<KF>(x, ldx, F, col, ck.y, ck.z, st, t_h, slope, dp, seed, acc);
   const int KP = H * Fp;
@@ -321,97 +454,185 @@ __global__ void __launch_bounds__(256) k_hub_partial(
     }
 }
 
-// Merge the chunks of each hub: M = max m_c, S = sum S_c e^(m_c - M),
-// z = sum z_c e^(m_c - M) / (S + eps).  One wave per hub.
-__global__ void __launch_bounds__(256) k_hub_merge(const float* __restrict__ part, int Fp,
+// Per hub: M_h = max_c m_ch, S_h = sum_c S_ch e^(m_ch - M_h).  One wave per hub,
+// lanes over chunks.  Writes hubstat[hub][16] and the backward stats.
+__global__ void __launch_bounds__(256) k_hub_stats(const float* __restrict__ part, int Fp,
                                                    const int32_t* __restrict__ chunk_ptr,
                                                    const int32_t* __restrict__ hub_dst,
-                                                   int64_t num_hubs, float* __restrict__ zhub,
+                                                   int64_t num_hubs, float* __restrict__ hubstat,
                                                    float* __restrict__ stats) {
   const int lane = threadIdx.x & 63;
   const int64_t hb = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   if (hb >= num_hubs) return;
-  const int KP = H * Fp;
+  const int64_t stride = 16 + int64_t(H) * Fp;
   const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
-  // lanes 0..7 own heads; everyone computes M and S for head (lane & 7)
-  const int h = lane & 7;
-  float M = -INFINITY;
-  for (int c = c0; c < c1; ++c) M = fmaxf(M, part[int64_t(c) * (16 + KP) + h]);
-  float S = 0.f;
-  for (int c = c0; c < c1; ++c) {
-    const float* pr = part + int64_t(c) * (16 + KP);
-    S += pr[8 + h] * __expf(pr[h] - M);
-  }
-  if (stats && lane < 8) {
+  float M[H], S[H];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) { M[hh] = -INFINITY; S[hh] = 0.f; }
+  for (int c = c0 + lane; c < c1; c += 64)
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) M[hh] = fmaxf(M[hh], part[c * stride + hh]);
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) M[hh] = fmaxf(M[hh], __shfl_xor(M[hh], o));
+  for (int c = c0 + lane; c < c1; c += 64)
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) S[hh] += part[c * stride + 8 + hh] * __expf(part[c * stride + hh] - M[hh]);
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) S[hh] += __shfl_xor(S[hh], o);
+  if (lane == 0) {
     const int64_t i = hub_dst[hb];
-    stats[i * 16 + lane] = M;
-    stats[i * 16 + 8 + lane] = S;
-  }
-  float* zr = zhub + hb * KP;
-  for (int k = lane; k < KP; k += 64) {
-    const int hh = k / Fp;
-    const float Mh = __shfl(M, hh);
-    const float inv = 1.0f / (__shfl(S, hh) + kSoftmaxEps);
-    float z = 0.f;
-    for (int c = c0; c < c1; ++c) {
-      const float* pr = part + int64_t(c) * (16 + KP);
-      z = fmaf(pr[16 + k], __expf(pr[hh] - Mh), z);
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) {
+      hubstat[hb * 16 + hh] = M[hh];
+      hubstat[hb * 16 + 8 + hh] = S[hh];
+      if (stats) {
+        stats[i * 16 + hh] = M[hh];
+        stats[i * 16 + 8 + hh] = S[hh];
+      }
     }
-    zr[k] = z * inv;
   }
 }
 
+// z = sum_c z_c e^(m_c - M) / (S + eps).  Grid (hubs, KP/64); 64 columns x 4
+// chunk lanes per block.
+__global__ void __launch_bounds__(256) k_hub_merge(const float* __restrict__ part, int Fp,
+                                                   const int32_t* __restrict__ chunk_ptr,
+                                                   const float* __restrict__ hubstat,
+                                                   float* __restrict__ zhub) {
+  __shared__ float sred[256];
+  const int tid = threadIdx.x;
+  const int64_t hb = blockIdx.x;
+  const int KP = H * Fp;
+  const int64_t stride = 16 + KP;
+  const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
+  const int k = blockIdx.y * 64 + (tid & 63);
+  const int cl = tid >> 6;
+  float zsum = 0.f;
+  int hh = 0;
+  if (k < KP) {
+    hh = k / Fp;
+    const float Mh = hubstat[hb * 16 + hh];
+    for (int c = c0 + cl; c < c1; c += 4) {
+      const float* pr = part + c * stride;
+      zsum = fmaf(pr[16 + k], __expf(pr[hh] - Mh), zsum);
+    }
+  }
+  sred[tid] = zsum;
+  __syncthreads();
+  if (cl == 0 && k < KP) {
+    const float zt = sred[tid] + sred[tid + 64] + sred[tid + 128] + sred[tid + 192];
+    zhub[hb * KP + k] = zt / (hubstat[hb * 16 + 8 + hh] + kSoftmaxEps);
+  }
+}
+
+// ---------------------------------------------------------------------------
 inline int kf_for(int F) { return (F + 63) / 64; }
 
-size_t fused_smem(int Fp) { return sizeof(float) * (kTile * (H * Fp + 4) + 4 * 64 * 4); }
+size_t fused_smem(int Fp) {
+  return sizeof(float) * (kTile * (4 * Fp + 4) + 2 * 3 * 4 * 64 * 4 + 2 * kTile);
+}
 
-template <int KF>
-gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const float* uv, int Fp,
+gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const float* uv, int Fu,
                          float* st, hipStream_t stream) {
   if (rows <= 0) return GFD_OK;
-  int64_t blocks = (rows + 3) / 4;
+  int64_t blocks = (rows + 63) / 64;  // 4 waves x 16 rows
   if (blocks > 8192) blocks = 8192;
-  k_logits<KF><<<int(blocks), 256, sizeof(float) * 16 * Fp, stream>>>(x, rows, F, ldx, uv, Fp, st);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(x);
+  if (a % 16 == 0 && ldx % 4 == 0)
+    k_logits<4><<<int(blocks), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
+  else if (a % 8 == 0 && ldx % 2 == 0)
+    k_logits<2><<<int(blocks), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
+  else
+    k_logits<1><<<int(blocks), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
 
+struct AggArgs {
+  const float* x; int F; int64_t ldx;
+  const int32_t* rowptr; const int32_t* col; int64_t num_dst; int64_t dst_offset;
+  const float* st; const char* packed; const float* bias; float slope; float dp; uint64_t seed;
+  gfd_plan plan; int stages; float* out; float* stats;
+  float* part; float* hubstat; float* zhub;
+};
+
 template <int KF>
-gfd_status launch_aggregate(const float* x, int F, int Fp, int64_t ldx, const int32_t* rowptr,
-                            const int32_t* col, int64_t num_dst, int64_t dst_offset,
-                            const float* st, const PackLayout& L, const char* packed,
-                            const float* bias, float slope, float dp, uint64_t seed,
-                            const int32_t* hub_rank, const int32_t* hub_chunk,
-                            const int32_t* hub_chunk_ptr, const int32_t* hub_dst,
-                            int64_t num_hubs, int64_t num_chunks, int stages, float* out,
-                            float* stats, float* part, float* zhub, hipStream_t stream) {
-  const int KP = H * Fp;
-  if (num_hubs > 0 && (stages & GFD_STAGE_HUBS)) {
-    int64_t blocks = (num_chunks + 3) / 4;
-    k_hub_partial<KF><<<int(blocks), 256, 0, stream>>>(x, F, Fp, ldx, col, dst_offset, st, slope,
-                                                       dp, seed,
-                                                       reinterpret_cast<const int4*>(hub_chunk),
-                                                       num_chunks, part);
+gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
+  const int Fp = L.Fp, KP = L.KP;
+  const gfd_plan& p = a.plan;
+  if (p.num_hubs > 0 && (a.stages & GFD_STAGE_HUBS)) {
+    int64_t blocks = (p.num_chunks + 3) / 4;
+    k_hub_partial<KF><<<int(blocks), 256, 0, stream>>>(
+        a.x, a.F, Fp, a.ldx, a.col, a.dst_offset, a.st, a.slope, a.dp, a.seed,
+        reinterpret_cast<const int4*>(p.hub_chunk), p.num_chunks, a.part);
     GFD_LAUNCH_CHECK();
-    k_hub_merge<<<int((num_hubs + 3) / 4), 256, 0, stream>>>(part, Fp, hub_chunk_ptr, hub_dst,
-                                                             num_hubs, zhub, stats);
+    k_hub_stats<<<int((p.num_hubs + 3) / 4), 256, 0, stream>>>(
+        a.part, Fp, p.hub_chunk_ptr, p.hub_dst, p.num_hubs, a.hubstat, a.stats);
+    GFD_LAUNCH_CHECK();
+    dim3 mg(unsigned(p.num_hubs), unsigned((KP + 63) / 64));
+    k_hub_merge<<<mg, 256, 0, stream>>>(a.part, Fp, p.hub_chunk_ptr, a.hubstat, a.zhub);
     GFD_LAUNCH_CHECK();
   }
-  (void)KP;
-  if (!(stages & GFD_STAGE_TILES)) return GFD_OK;
-  const int64_t tiles = (num_dst + kTile - 1) / kTile;
-  if (tiles > 0x7fffffff) return GFD_ERR_UNSUPPORTED;
-  const uint4* whi = reinterpret_cast<const uint4*>(packed + L.whi_off);
-  const uint4* wlo = reinterpret_cast<const uint4*>(packed + L.wlo_off);
-  k_fused<KF><<<int(tiles), kFusedThreads, fused_smem(Fp), stream>>>(
-      x, F, Fp, ldx, rowptr, col, num_dst, dst_offset, st, whi, wlo, bias, slope, dp, seed,
-      num_hubs > 0 ? hub_rank : nullptr, zhub, out, stats);
+  if (!(a.stages & GFD_STAGE_TILES)) return GFD_OK;
+  const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
+  const PackHeader* hdr = reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off);
+  const uint4* whi = reinterpret_cast<const uint4*>(a.packed + L.whi_off);
+  const uint4* wlo = reinterpret_cast<const uint4*>(a.packed + L.wlo_off);
+  k_fused<KF><<<int(tiles), kFusedWaves * 64, fused_smem(Fp), stream>>>(
+      a.x, a.F, Fp, a.ldx, a.rowptr, a.col, a.num_dst, a.dst_offset, p.row_order, a.st, hdr,
+      whi, wlo, a.bias, a.slope, a.dp, a.seed, p.num_hubs > 0 ? p.hub_rank : nullptr, a.zhub,
+      a.out, a.stats);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
 
 bool check_hc(int heads, int channels, int F) {
   return heads == H && channels == C && F >= 1 && F <= 256;
+}
+
+gfd_status aggregate_impl(const AggArgs& a, hipStream_t stream) {
+  PackLayout L = pack_layout(a.F);
+  switch (kf_for(a.F)) {
+    case 1: return launch_aggregate<1>(a, L, stream);
+    case 2: return launch_aggregate<2>(a, L, stream);
+    case 3: return launch_aggregate<3>(a, L, stream);
+    case 4: return launch_aggregate<4>(a, L, stream);
+    default: return GFD_ERR_UNSUPPORTED;
+  }
+}
+
+gfd_status check_agg_args(const float* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
+                          const int32_t* col, int64_t num_dst, int64_t dst_offset, float dp,
+                          const gfd_plan& p, float* out) {
+  if (N <= 0 || num_dst < 0 || dst_offset < 0 || dst_offset + num_dst > N) return GFD_ERR_ARGUMENT;
+  if (!x || !rowptr || !col || !out || ldx < F) return GFD_ERR_ARGUMENT;
+  if (!(dp >= 0.f && dp < 1.f)) return GFD_ERR_ARGUMENT;
+  if (p.num_hubs < 0 || p.num_chunks < 0 || p.num_hubs > 0x7fffffff) return GFD_ERR_ARGUMENT;
+  if (p.num_hubs > 0 &&
+      (!p.hub_rank || !p.hub_chunk || !p.hub_chunk_ptr || !p.hub_dst || p.num_chunks <= 0))
+    return GFD_ERR_ARGUMENT;
+  if ((num_dst + kTile - 1) / kTile > 0x7fffffff) return GFD_ERR_UNSUPPORTED;
+  return GFD_OK;
+}
+
+gfd_plan plan_or_empty(const gfd_plan* p) {
+  if (p) return *p;
+  gfd_plan e;
+  e.row_order = e.hub_rank = e.hub_chunk = e.hub_chunk_ptr = e.hub_dst = nullptr;
+  e.num_hubs = e.num_chunks = 0;
+  return e;
+}
+
+size_t hub_ws_layout(Carve* c, int64_t num_hubs, int64_t num_chunks, const PackLayout& L,
+                     float** part, float** hubstat, float** zhub) {
+  *part = c->take<float>(size_t(num_chunks) * (16 + L.KP));
+  *hubstat = c->take<float>(size_t(num_hubs) * 16);
+  *zhub = c->take<float>(size_t(num_hubs) * L.KP);
+  return c->off;
 }
 
 }  // namespace
@@ -431,12 +652,15 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   if (!weight || !att_src || !att_dst || !packed) return GFD_ERR_ARGUMENT;
   PackLayout L = pack_layout(F);
   char* p = static_cast<char*>(packed);
-  int n_uv = 2 * H * L.Fp;
-  k_pack_uv<<<(n_uv + 255) / 256, 256, 0, stream>>>(weight, att_src, att_dst, F, L.Fp,
+  PackHeader* hdr = reinterpret_cast<PackHeader*>(p + L.hdr_off);
+  k_wmax<<<1, 256, 0, stream>>>(weight, H * C * F, hdr);
+  GFD_LAUNCH_CHECK();
+  int n_uv = 2 * H * L.Fu;
+  k_pack_uv<<<(n_uv + 255) / 256, 256, 0, stream>>>(weight, att_src, att_dst, F, L.Fu,
                                                     reinterpret_cast<float*>(p + L.uv_off));
   GFD_LAUNCH_CHECK();
   int n_fr = L.KS * 4 * 64;
-  k_pack_frag<<<(n_fr + 255) / 256, 256, 0, stream>>>(weight, F, L.Fp, L.KS,
+  k_pack_frag<<<(n_fr + 255) / 256, 256, 0, stream>>>(weight, F, L.Fp, L.KS, hdr,
                                                       reinterpret_cast<uint4*>(p + L.whi_off),
                                                       reinterpret_cast<uint4*>(p + L.wlo_off));
   GFD_LAUNCH_CHECK();
@@ -450,12 +674,7 @@ gfd_status gfd_gat_logits(const float* x, int64_t rows, int F, int64_t ldx, cons
   if (rows < 0 || (rows > 0 && (!x || !packed || !st)) || ldx < F) return GFD_ERR_ARGUMENT;
   PackLayout L = pack_layout(F);
   const float* uv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + L.uv_off);
-  switch (kf_for(F)) {
-    case 1: return launch_logits<1>(x, rows, F, ldx, uv, L.Fp, st, stream);
-    case 2: return launch_logits<2>(x, rows, F, ldx, uv, L.Fp, st, stream);
-    case 3: return launch_logits<3>(x, rows, F, ldx, uv, L.Fp, st, stream);
-    default: return launch_logits<4>(x, rows, F, ldx, uv, L.Fp, st, stream);
-  }
+  return launch_logits(x, rows, F, ldx, uv, L.Fu, st, stream);
 }
 
 size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int heads,
@@ -464,114 +683,67 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int
   (void)num_dst;
   PackLayout L = pack_layout(F);
   Sizer s;
+  s.take<float>(size_t(num_chunks) * (16 + L.KP));    // hub partials
+  s.take<float>(size_t(num_hubs) * 16);               // per-hub (max, sum)
+  s.take<float>(size_t(num_hubs) * L.KP);             // merged hub z rows
   s.take<char>(L.bytes);                              // packed weights (gfd_gat_fwd only)
   s.take<float>(size_t(num_nodes) * 16);              // st (gfd_gat_fwd when st == NULL)
-  s.take<float>(size_t(num_chunks) * (16 + L.KP));    // hub partials
-  s.take<float>(size_t(num_hubs) * L.KP);             // merged hub z rows
   return s.off;
-}
-
-static gfd_status aggregate_impl(const float* x, int64_t N, int F, int64_t ldx,
-                                 const int32_t* rowptr, const int32_t* col, int64_t num_dst,
-                                 int64_t dst_offset, const float* st, const void* packed,
-                                 const float* bias, float slope, float dp, uint64_t seed,
-                                 const int32_t* hub_rank, const int32_t* hub_chunk,
-                                 const int32_t* hub_chunk_ptr, const int32_t* hub_dst,
-                                 int64_t num_hubs, int64_t num_chunks, int stages, float* out,
-                                 float* stats, float* part, float* zhub, hipStream_t stream) {
-  PackLayout L = pack_layout(F);
-  const char* pk = static_cast<const char*>(packed);
-  switch (kf_for(F)) {
-#define GFD_AGG(KF)                                                                              \
-  case KF:                                                                                       \
-    return launch_aggregate<KF>(x, F, L.Fp, ldx, rowptr, col, num_dst, dst_offset, st, L, pk,    \
-                                bias, slope, dp, seed, hub_rank, hub_chunk, hub_chunk_ptr,       \
-                                hub_dst, num_hubs, num_chunks, stages, out, stats, part, zhub,   \
-                                stream);
-    GFD_AGG(1)
-    GFD_AGG(2)
-    GFD_AGG(3)
-    GFD_AGG(4)
-#undef GFD_AGG
-    default: return GFD_ERR_UNSUPPORTED;
-  }
-  (void)N;
-}
-
-static gfd_status check_agg_args(const float* x, int64_t N, int F, int64_t ldx,
-                                 const int32_t* rowptr, const int32_t* col, int64_t num_dst,
-                                 int64_t dst_offset, float dp, const int32_t* hub_rank,
-                                 const int32_t* hub_chunk, const int32_t* hub_chunk_ptr,
-                                 const int32_t* hub_dst, int64_t num_hubs, int64_t num_chunks,
-                                 float* out) {
-  if (N <= 0 || num_dst < 0 || dst_offset < 0 || dst_offset + num_dst > N) return GFD_ERR_ARGUMENT;
-  if (!x || !rowptr || !col || !out || ldx < F) return GFD_ERR_ARGUMENT;
-  if (!(dp >= 0.f && dp < 1.f)) return GFD_ERR_ARGUMENT;
-  if (num_hubs < 0 || num_chunks < 0) return GFD_ERR_ARGUMENT;
-  if (num_hubs > 0 && (!hub_rank || !hub_chunk || !hub_chunk_ptr || !hub_dst || num_chunks <= 0))
-    return GFD_ERR_ARGUMENT;
-  return GFD_OK;
 }
 
 gfd_status gfd_gat_aggregate(const float* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
                              const int32_t* col, int64_t num_dst, int64_t dst_offset,
                              const float* st, const void* packed, const float* bias, int heads,
                              int channels, float slope, float dp, uint64_t seed,
-                             const int32_t* hub_rank, const int32_t* hub_chunk,
-                             const int32_t* hub_chunk_ptr, const int32_t* hub_dst,
-                             int64_t num_hubs, int64_t num_chunks, int stages, float* out,
-                             float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+                             const gfd_plan* plan, int stages, float* out, float* stats, void* ws,
+                             size_t ws_bytes, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
-  gfd_status a = check_agg_args(x, N, F, ldx, rowptr, col, num_dst, dst_offset, dp, hub_rank,
-                                hub_chunk, hub_chunk_ptr, hub_dst, num_hubs, num_chunks, out);
-  if (a != GFD_OK) return a;
+  gfd_plan p = plan_or_empty(plan);
+  gfd_status s = check_agg_args(x, N, F, ldx, rowptr, col, num_dst, dst_offset, dp, p, out);
+  if (s != GFD_OK) return s;
   if (!st || !packed || stages < 1 || stages > 3) return GFD_ERR_ARGUMENT;
   if (num_dst == 0) return GFD_OK;
   PackLayout L = pack_layout(F);
-  Carve c(ws, ws_bytes);
-  float* part = nullptr;
-  float* zhub = nullptr;
-  if (num_hubs > 0) {
-    part = c.take<float>(size_t(num_chunks) * (16 + L.KP));
-    zhub = c.take<float>(size_t(num_hubs) * L.KP);
+  AggArgs a{x, F, ldx, rowptr, col, num_dst, dst_offset, st, static_cast<const char*>(packed),
+            bias, slope, dp, seed, p, stages, out, stats, nullptr, nullptr, nullptr};
+  if (p.num_hubs > 0) {
+    Carve c(ws, ws_bytes);
+    hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.hubstat, &a.zhub);
     if (!c.ok) return GFD_ERR_WORKSPACE;
   }
-  return aggregate_impl(x, N, F, ldx, rowptr, col, num_dst, dst_offset, st, packed, bias, slope,
-                        dp, seed, hub_rank, hub_chunk, hub_chunk_ptr, hub_dst, num_hubs,
-                        num_chunks, stages, out, stats, part, zhub, stream);
+  return aggregate_impl(a, stream);
 }
 
 gfd_status gfd_gat_fwd(const float* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
                        const int32_t* col, const float* weight, const float* att_src,
                        const float* att_dst, const float* bias, int heads, int channels,
-                       float slope, float dp, uint64_t seed, const int32_t* hub_rank,
-                       const int32_t* hub_chunk, const int32_t* hub_chunk_ptr,
-                       const int32_t* hub_dst, int64_t num_hubs, int64_t num_chunks, float* out,
+                       float slope, float dp, uint64_t seed, const gfd_plan* plan, float* out,
                        float* st, float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
-  gfd_status a = check_agg_args(x, N, F, ldx, rowptr, col, N, 0, dp, hub_rank, hub_chunk,
-                                hub_chunk_ptr, hub_dst, num_hubs, num_chunks, out);
-  if (a != GFD_OK) return a;
+  gfd_plan p = plan_or_empty(plan);
+  gfd_status s = check_agg_args(x, N, F, ldx, rowptr, col, N, 0, dp, p, out);
+  if (s != GFD_OK) return s;
   if (!weight || !att_src || !att_dst) return GFD_ERR_ARGUMENT;
-  if (ws_bytes < gfd_gat_fwd_workspace_size(N, N, F, heads, channels, num_hubs, num_chunks))
+  if (ws_bytes < gfd_gat_fwd_workspace_size(N, N, F, heads, channels, p.num_hubs, p.num_chunks))
     return GFD_ERR_WORKSPACE;
   PackLayout L = pack_layout(F);
   Carve c(ws, ws_bytes);
+  AggArgs a{x, F, ldx, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p, GFD_STAGE_ALL,
+            out, stats, nullptr, nullptr, nullptr};
+  hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.hubstat, &a.zhub);
   void* packed = c.take<char>(L.bytes);
   float* st_ws = c.take<float>(size_t(N) * 16);
-  float* part = c.take<float>(size_t(num_chunks) * (16 + L.KP));
-  float* zhub = c.take<float>(size_t(num_hubs) * L.KP);
   if (!c.ok) return GFD_ERR_WORKSPACE;
   if (st == nullptr) st = st_ws;
-  gfd_status s = gfd_gat_pack_weights(weight, att_src, att_dst, F, heads, channels, packed, stream_);
+  a.st = st;
+  a.packed = static_cast<const char*>(packed);
+  s = gfd_gat_pack_weights(weight, att_src, att_dst, F, heads, channels, packed, stream_);
   if (s != GFD_OK) return s;
   s = gfd_gat_logits(x, N, F, ldx, packed, heads, channels, st, stream_);
   if (s != GFD_OK) return s;
-  return aggregate_impl(x, N, F, ldx, rowptr, col, N, 0, st, packed, bias, slope, dp, seed,
-                        hub_rank, hub_chunk, hub_chunk_ptr, hub_dst, num_hubs, num_chunks,
-                        GFD_STAGE_ALL, out, stats, part, zhub, stream);
+  return aggregate_impl(a, stream);
 }
 
 }  // extern "C"

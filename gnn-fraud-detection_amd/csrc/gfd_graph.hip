@@ -137,6 +137,17 @@ __global__ void k_hub_tail(const int32_t* __restrict__ hub_idx, const int32_t* _
   if (nh <= max_hubs && hub_chunk_ptr != nullptr) hub_chunk_ptr[nh] = nc;
 }
 
+// order keys: rows with more messages first (key = cap + 1 - min(deg, cap + 1)).
+__global__ void k_order_keys(const int32_t* __restrict__ rowptr, int64_t n, int32_t cap,
+                             uint32_t* __restrict__ key, int32_t* __restrict__ val) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    int32_t d = rowptr[i + 1] - rowptr[i];
+    key[i] = uint32_t(cap + 1 - min(d, cap + 1));
+    val[i] = int32_t(i);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -335,6 +346,44 @@ gfd_status gfd_plan_hubs(const int32_t* rowptr, int64_t n, int32_t thr, int32_t 
   *num_hubs = h[0];
   *num_chunks = h[1];
   if (h[0] > max_hubs || h[1] > max_chunks) return GFD_ERR_WORKSPACE;
+  return GFD_OK;
+}
+
+static size_t order_layout(int64_t n, int32_t cap, size_t* sort_tmp_out) {
+  size_t sort_tmp = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, sort_tmp, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (int32_t*)nullptr, (int32_t*)nullptr, size_t(n > 0 ? n : 1), 0,
+                                  bits_for(int64_t(cap) + 1));
+  if (sort_tmp_out) *sort_tmp_out = sort_tmp;
+  Sizer s;
+  s.take<uint32_t>(n); s.take<uint32_t>(n); s.take<int32_t>(n); s.take<char>(sort_tmp);
+  return s.off;
+}
+
+size_t gfd_order_workspace_size(int64_t num_dst, int32_t cap) {
+  if (num_dst <= 0 || cap < 1) return 0;
+  return order_layout(num_dst, cap, nullptr);
+}
+
+gfd_status gfd_plan_order(const int32_t* rowptr, int64_t n, int32_t cap, int32_t* order, void* ws,
+                          size_t ws_bytes, gfd_stream_t stream_) {
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (n <= 0 || cap < 1 || !rowptr || !order) return GFD_ERR_ARGUMENT;
+  size_t sort_tmp;
+  size_t need = order_layout(n, cap, &sort_tmp);
+  if (ws == nullptr || ws_bytes < need) return GFD_ERR_WORKSPACE;
+  Carve c(ws, ws_bytes);
+  uint32_t* kin = c.take<uint32_t>(n);
+  uint32_t* kout = c.take<uint32_t>(n);
+  int32_t* vin = c.take<int32_t>(n);
+  void* sort_buf = c.take<char>(sort_tmp);
+  if (!c.ok) return GFD_ERR_WORKSPACE;
+  k_order_keys<<<grid_for(n), kBlock, 0, stream>>>(rowptr, n, cap, kin, vin);
+  GFD_LAUNCH_CHECK();
+  size_t st = sort_tmp;
+  if (rocprim::radix_sort_pairs(sort_buf, st, kin, kout, vin, order, size_t(n), 0,
+                                bits_for(int64_t(cap) + 1), stream) != hipSuccess)
+    return GFD_ERR_HIP;
   return GFD_OK;
 }
 

@@ -17,6 +17,16 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgfd.so")
 c_i32, c_i64, c_u64, c_f32, c_sz = ct.c_int32, ct.c_int64, ct.c_uint64, ct.c_float, ct.c_size_t
 P = ct.c_void_p
 
+
+
+class GfdPlan(ct.Structure):
+    """``gfd_plan`` (include/gfd.h)."""
+    _fields_ = [("row_order", P), ("hub_rank", P), ("hub_chunk", P), ("hub_chunk_ptr", P),
+                ("hub_dst", P), ("num_hubs", c_i64), ("num_chunks", c_i64)]
+
+
+PLAN = ct.POINTER(GfdPlan)
+
 # name -> (restype, argtypes); mirrors include/gfd.h one to one
 SIGNATURES = {
     "gfd_status_string": (ct.c_char_p, [c_i32]),
@@ -28,16 +38,18 @@ SIGNATURES = {
     "gfd_plan_workspace_size": (c_sz, [c_i64]),
     "gfd_plan_hubs": (c_i32, [P, c_i64, c_i32, c_i32, P, P, P, P, c_i64, c_i64,
                               ct.POINTER(c_i64), ct.POINTER(c_i64), P, c_sz, P]),
+    "gfd_order_workspace_size": (c_sz, [c_i64, c_i32]),
+    "gfd_plan_order": (c_i32, [P, c_i64, c_i32, P, P, c_sz, P]),
     "gfd_gat_packed_size": (c_sz, [ct.c_int, ct.c_int, ct.c_int]),
     "gfd_gat_pack_weights": (c_i32, [P, P, P, ct.c_int, ct.c_int, ct.c_int, P, P]),
     "gfd_gat_logits": (c_i32, [P, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),
     "gfd_gat_fwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int, c_i64,
                                           c_i64]),
     "gfd_gat_aggregate": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P, P, P,
-                                  ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, c_i64,
-                                  c_i64, ct.c_int, P, P, P, c_sz, P]),
+                                  ct.c_int, ct.c_int, c_f32, c_f32, c_u64, PLAN, ct.c_int, P, P,
+                                  P, c_sz, P]),
     "gfd_gat_fwd": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int, ct.c_int,
-                            c_f32, c_f32, c_u64, P, P, P, P, c_i64, c_i64, P, P, P, P, c_sz, P]),
+                            c_f32, c_f32, c_u64, PLAN, P, P, P, P, c_sz, P]),
     "gfd_gat_bwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int]),
     "gfd_gat_bwd": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, P, ct.c_int,
                             ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, P, P, P, P, P, c_sz, P]),

@@ -30,40 +30,70 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 
 
 @dataclass
-class HubPlan:
-    hub_rank: torch.Tensor
+class Plan:
+    """Execution plan of one destination range (``gfd_plan``): the tile order
+    (destinations by descending message count) and the hub split."""
+    num_dst: int
+    row_order: Optional[torch.Tensor]
+    hub_rank: Optional[torch.Tensor]
     hub_chunk: Optional[torch.Tensor]
     hub_chunk_ptr: Optional[torch.Tensor]
     hub_dst: Optional[torch.Tensor]
     num_hubs: int
     num_chunks: int
+    _c: object = field(default=None, repr=False)
 
-    def args(self):
+    def cstruct(self):
+        """ctypes pointer to a gfd_plan mirroring this object (kept alive here)."""
+        if self._c is None:
+            p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+            hubs = self.num_hubs > 0
+            self._c = _lib.GfdPlan(p(self.row_order), p(self.hub_rank) if hubs else None,
+                                   p(self.hub_chunk) if hubs else None,
+                                   p(self.hub_chunk_ptr) if hubs else None,
+                                   p(self.hub_dst) if hubs else None, self.num_hubs,
+                                   self.num_chunks)
+        return _lib.ct.byref(self._c)
+
+    def hub_messages(self) -> int:
         if self.num_hubs == 0:
-            return (None, None, None, None, 0, 0)
-        return (self.hub_rank.data_ptr(), self.hub_chunk.data_ptr(), self.hub_chunk_ptr.data_ptr(),
-                self.hub_dst.data_ptr(), self.num_hubs, self.num_chunks)
+            return 0
+        ck = self.hub_chunk.view(-1, 4)
+        return int((ck[:, 2] - ck[:, 1]).sum().item())
 
 
-def plan_hubs(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
-              chunk: int = HUB_CHUNK) -> HubPlan:
-    """Hub plan for the destination range described by ``rowptr`` ([n+1] int32)."""
+def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
+               chunk: int = HUB_CHUNK, order: bool = True) -> Plan:
+    """Plan for the destination range described by ``rowptr`` ([n+1] int32)."""
     n = rowptr.numel() - 1
     dev = rowptr.device
+    lib = _lib.load()
+    stream = _lib.stream_handle(dev)
     max_hubs = num_messages // (threshold + 1) + 1
     max_chunks = num_messages // chunk + max_hubs + 1
     hub_rank = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     hub_chunk = torch.empty(4 * max_chunks, dtype=torch.int32, device=dev)
     hub_chunk_ptr = torch.empty(max_hubs + 1, dtype=torch.int32, device=dev)
     hub_dst = torch.empty(max_hubs, dtype=torch.int32, device=dev)
-    ws = _ws(_lib.load().gfd_plan_workspace_size(n), dev)
+    ws = _ws(lib.gfd_plan_workspace_size(n), dev)
     nh, nc = _lib.c_i64(0), _lib.c_i64(0)
     _lib.call("gfd_plan_hubs", rowptr.data_ptr(), n, threshold, chunk, hub_rank.data_ptr(),
               hub_chunk.data_ptr(), hub_chunk_ptr.data_ptr(), hub_dst.data_ptr(), max_hubs,
-              max_chunks, _lib.ct.byref(nh), _lib.ct.byref(nc), ws.data_ptr(), ws.numel(),
-              _lib.stream_handle(dev))
-    return HubPlan(hub_rank, hub_chunk[:4 * nc.value], hub_chunk_ptr[:nh.value + 1],
-                   hub_dst[:nh.value], nh.value, nc.value)
+              max_chunks, _lib.ct.byref(nh), _lib.ct.byref(nc), ws.data_ptr(), ws.numel(), stream)
+    row_order = None
+    if order and n > 0:
+        row_order = torch.empty(n, dtype=torch.int32, device=dev)
+        ws = _ws(lib.gfd_order_workspace_size(n, threshold), dev)
+        _lib.call("gfd_plan_order", rowptr.data_ptr(), n, threshold, row_order.data_ptr(),
+                  ws.data_ptr(), ws.numel(), stream)
+    return Plan(n, row_order, hub_rank, hub_chunk[:4 * nc.value], hub_chunk_ptr[:nh.value + 1],
+                hub_dst[:nh.value], nh.value, nc.value)
+
+
+# backwards-compatible name
+def plan_hubs(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
+              chunk: int = HUB_CHUNK) -> Plan:
+    return build_plan(rowptr, num_messages, threshold, chunk)
 
 
 @dataclass
@@ -81,17 +111,17 @@ class CSRGraph:
     col: torch.Tensor         # int32 [E'] (source ids)
     num_messages: int         # E' = E - self loops + N
     num_input_edges: int
-    _hubs: Optional[HubPlan] = field(default=None, repr=False)
+    _plan: Optional[Plan] = field(default=None, repr=False)
     _csc: Optional[CSC] = field(default=None, repr=False)
 
     @property
     def device(self):
         return self.rowptr.device
 
-    def hubs(self) -> HubPlan:
-        if self._hubs is None:
-            self._hubs = plan_hubs(self.rowptr, self.num_messages)
-        return self._hubs
+    def plan(self) -> Plan:
+        if self._plan is None:
+            self._plan = build_plan(self.rowptr, self.num_messages)
+        return self._plan
 
     def csc(self) -> CSC:
         if self._csc is None:
@@ -110,7 +140,7 @@ class CSRGraph:
         """Destination range [lo, hi): a rowptr view (absolute positions into col)."""
         rp = self.rowptr[lo:hi + 1]
         m = int(self.rowptr[hi].item()) - int(self.rowptr[lo].item())
-        return CSRShard(self, lo, hi, rp, plan_hubs(rp, m))
+        return CSRShard(self, lo, hi, rp, m, build_plan(rp, m))
 
 
 @dataclass
@@ -119,7 +149,8 @@ class CSRShard:
     lo: int
     hi: int
     rowptr: torch.Tensor
-    hubs: HubPlan
+    num_messages: int
+    plan: Plan
 
 
 def csr_from_coo(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
@@ -145,15 +176,18 @@ def csr_from_coo(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
     return CSRGraph(num_nodes, rowptr, col[:M], M, E)
 
 
-_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_CACHE: dict = {}
 
 
 def get_graph(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
-    """Cached ``csr_from_coo`` keyed on the tensor object, its version and N."""
+    """Cached ``csr_from_coo`` keyed on the tensor object (held weakly), its
+    in-place version counter, storage pointer, shape and N."""
     key = (edge_index._version, int(num_nodes), edge_index.data_ptr(), tuple(edge_index.shape))
-    ent = _CACHE.get(edge_index)
-    if ent is not None and ent[0] == key:
-        return ent[1]
+    ent = _CACHE.get(id(edge_index))
+    if ent is not None and ent[0]() is edge_index and ent[1] == key:
+        return ent[2]
     g = csr_from_coo(edge_index, num_nodes)
-    _CACHE[edge_index] = (key, g)
+    oid = id(edge_index)
+    ref = weakref.ref(edge_index, lambda _r, oid=oid: _CACHE.pop(oid, None))
+    _CACHE[oid] = (ref, key, g)
     return g

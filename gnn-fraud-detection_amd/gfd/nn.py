@@ -54,17 +54,17 @@ class GATConvFunction(torch.autograd.Function):
         N, F = x.shape
         HC = weight.size(0)
         H, C = SUPPORTED_HEADS, HC // SUPPORTED_HEADS
-        hubs = graph.hubs()
+        plan = graph.plan()
         need_stats = any(ctx.needs_input_grad[:5])
         out = torch.empty((N, C), dtype=torch.float32, device=dev)
         st = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         stats = torch.empty((N, 2 * H), dtype=torch.float32, device=dev) if need_stats else None
         lib = _lib.load()
-        ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, hubs.num_hubs, hubs.num_chunks), dev)
+        ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, plan.num_hubs, plan.num_chunks), dev)
         _lib.call("gfd_gat_fwd", x.data_ptr(), N, F, F, graph.rowptr.data_ptr(),
                   graph.col.data_ptr(), weight.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(),
                   _lib.ptr(bias), H, C, float(negative_slope), float(dropout_p),
-                  int(seed) & (2 ** 64 - 1), *hubs.args(), out.data_ptr(), st.data_ptr(),
+                  int(seed) & (2 ** 64 - 1), plan.cstruct(), out.data_ptr(), st.data_ptr(),
                   _lib.ptr(stats), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
         if need_stats:
             ctx.save_for_backward(x, weight, att_src, att_dst, st, stats)

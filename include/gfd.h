@@ -18,8 +18,9 @@
  *    nothing and keeps no global state.  All work is enqueued on ``stream``;
  *    nothing synchronises except where a function says so.
  *  - Floating point is IEEE fp32 at the boundary.  Internally the feature
- *    projection runs on bf16 MFMA with a 3-term hi/lo split (fp32-faithful to
- *    ~1e-6 relative); softmax, aggregation and accumulation are fp32.
+ *    projection runs on f16 MFMA with a 3-term hi/lo split over power-of-two
+ *    scaled rows (~2^-21 relative, fp32-faithful); logits are exact fp32 MFMA;
+ *    softmax, aggregation and accumulation are fp32.
  *  - Graph layout: ``edge_index`` is the reference's COO ``int64 [2, E]``
  *    (dataset.py:104; row 0 = source j, row 1 = destination i, flow
  *    source->target).  Internally a destination-sorted CSR of int32 with the
@@ -88,6 +89,13 @@ gfd_status gfd_plan_hubs(const int32_t* rowptr, int64_t num_dst, int32_t hub_thr
                          int64_t max_chunks, int64_t* num_hubs, int64_t* num_chunks, void* ws,
                          size_t ws_bytes, gfd_stream_t stream);
 
+/* Tile order: destination ids sorted by descending message count (capped at
+ * cap + 1, stable), so each 16-destination tile of the fused kernel holds rows
+ * of similar length (no tile waits on one long row).  order[num_dst]. */
+size_t gfd_order_workspace_size(int64_t num_dst, int32_t cap);
+gfd_status gfd_plan_order(const int32_t* rowptr, int64_t num_dst, int32_t cap, int32_t* order,
+                          void* ws, size_t ws_bytes, gfd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * GATConv forward (PyG GATConv.forward, concat=False, add_self_loops=True,
  * bias=True; gat.py:80 / tgn.py:94):
@@ -113,19 +121,30 @@ gfd_status gfd_gat_logits(const float* x, int64_t num_rows, int in_features, int
                           const void* packed, int heads, int channels, float* st,
                           gfd_stream_t stream);
 
+/* Execution plan of one destination range (all device pointers; NULL plan =
+ * identity order, no hubs).  Built once per graph by gfd_plan_order and
+ * gfd_plan_hubs on the range's rowptr. */
+typedef struct gfd_plan {
+  const int32_t* row_order;     /* [num_dst] tile order, or NULL for 0..num_dst-1      */
+  const int32_t* hub_rank;      /* [num_dst] -1 or hub index (NULL iff num_hubs == 0)  */
+  const int32_t* hub_chunk;     /* [4*num_chunks] {hub, e_begin, e_end, dst}           */
+  const int32_t* hub_chunk_ptr; /* [num_hubs + 1]                                      */
+  const int32_t* hub_dst;       /* [num_hubs]                                          */
+  int64_t num_hubs;
+  int64_t num_chunks;
+} gfd_plan;
+
 /* Workspace for gfd_gat_aggregate / gfd_gat_fwd (device bytes). */
 size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int in_features, int heads,
                                   int channels, int64_t num_hubs, int64_t num_chunks);
 
 /* Fused softmax-aggregate-project for destinations [dst_offset, dst_offset+num_dst)
- * whose CSR slice is rowptr[0..num_dst] (absolute positions into col), sources
- * are global rows of x (N rows, "halo resident").  st holds logits for all N
- * rows.  Hub arrays come from gfd_plan_hubs on the same rowptr (NULL with
- * num_hubs = 0 when no destination exceeds the threshold).
- * dropout_p > 0 applies dropout to alpha with a counter-based mask keyed by
- * (seed, CSR position, head) -- reproducible in the backward.
- * out [num_dst, C]; stats (nullable) [num_dst, 2H] = per-head softmax max and
- * denominator (sum of exp, without the eps), saved for the backward.
+ * whose CSR slice is rowptr[0..num_dst] (absolute positions into col); sources
+ * are global rows of x (N rows, "halo resident"); st holds logits for all N
+ * rows (gfd_gat_logits).  dropout_p > 0 applies dropout to alpha with a
+ * counter-based mask keyed by (seed, CSR position, head) -- reproducible in the
+ * backward.  out [num_dst, C]; stats (nullable) [num_dst, 2H] = per-head
+ * softmax max and denominator (sum of exp, without the eps) for the backward.
  * ``stages`` selects GFD_STAGE_HUBS (chunk partials + merge into ws),
  * GFD_STAGE_TILES (the fused tile kernel, reading merged hub rows from ws) or
  * GFD_STAGE_ALL; split calls must pass the same ws. */
@@ -136,22 +155,18 @@ gfd_status gfd_gat_aggregate(const float* x, int64_t num_nodes, int in_features,
                              const int32_t* rowptr, const int32_t* col, int64_t num_dst,
                              int64_t dst_offset, const float* st, const void* packed,
                              const float* bias, int heads, int channels, float negative_slope,
-                             float dropout_p, uint64_t dropout_seed, const int32_t* hub_rank,
-                             const int32_t* hub_chunk, const int32_t* hub_chunk_ptr,
-                             const int32_t* hub_dst, int64_t num_hubs, int64_t num_chunks,
+                             float dropout_p, uint64_t dropout_seed, const gfd_plan* plan,
                              int stages, float* out, float* stats, void* ws, size_t ws_bytes,
                              gfd_stream_t stream);
 
 /* One-call GATConv forward over the whole graph (num_dst = N, offset 0):
- * pack weights + logits + aggregate.  ws must hold
- * gfd_gat_fwd_workspace_size(N, N, F, H, C, num_hubs, num_chunks). */
+ * pack weights + logits + aggregate.  st (nullable, [N, 2H]) receives the
+ * logits; ws must hold gfd_gat_fwd_workspace_size(N, N, F, H, C, hubs, chunks). */
 gfd_status gfd_gat_fwd(const float* x, int64_t num_nodes, int in_features, int64_t x_stride,
                        const int32_t* rowptr, const int32_t* col, const float* weight,
                        const float* att_src, const float* att_dst, const float* bias, int heads,
                        int channels, float negative_slope, float dropout_p, uint64_t dropout_seed,
-                       const int32_t* hub_rank, const int32_t* hub_chunk,
-                       const int32_t* hub_chunk_ptr, const int32_t* hub_dst, int64_t num_hubs,
-                       int64_t num_chunks, float* out, float* st, float* stats, void* ws,
+                       const gfd_plan* plan, float* out, float* st, float* stats, void* ws,
                        size_t ws_bytes, gfd_stream_t stream);
 
 /* ---------------------------------------------------------------------------

@@ -70,12 +70,15 @@ def segment_softmax(alpha: torch.Tensor, index: torch.Tensor, num_nodes: int) ->
 def gatconv_forward(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Tensor,
                     att_src: torch.Tensor, att_dst: torch.Tensor, bias: Optional[torch.Tensor],
                     heads: int = 8, negative_slope: float = NEG_SLOPE, dropout: float = 0.0,
-                    training: bool = False, return_stats: bool = False):
+                    training: bool = False, return_stats: bool = False,
+                    alpha_mask: Optional[torch.Tensor] = None):
     """Functional PyG-dataflow GATConv (concat=False). Differentiable by autograd.
 
     ``weight`` is ``lin_src.weight`` ``[H*C, F]``; ``att_*`` are ``[1, H, C]``.
     With ``return_stats`` also returns the edge list with self loops, the
     per-(node, head) softmax max and sum, and the un-dropped alpha.
+    ``alpha_mask`` ([E', H], already scaled by 1/(1-p)) replaces F.dropout so a
+    test can impose the exact mask the device drew.
     """
     N = x.size(0)
     H = heads
@@ -87,7 +90,8 @@ def gatconv_forward(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Ten
     j, i = ei[0], ei[1]
     logit = F.leaky_relu(a_src.index_select(0, j) + a_dst.index_select(0, i), negative_slope)
     alpha = segment_softmax(logit, i, N)
-    alpha_d = F.dropout(alpha, p=dropout, training=training)
+    alpha_d = alpha * alpha_mask if alpha_mask is not None else \
+        F.dropout(alpha, p=dropout, training=training)
     msg = alpha_d.unsqueeze(-1) * h.index_select(0, j)     # [E', H, C]
     agg = torch.zeros((N, H, C), dtype=x.dtype).index_add(0, i, msg)
     out = agg.mean(dim=1)
