@@ -27,7 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
     if (hipGetLastError() != hipSuccess) return GFD_ERR_HIP; \
   } while (0)
 
-inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+__host__ __device__ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // Bump allocator over a caller-provided workspace.
 struct Carve {

@@ -15,6 +15,10 @@
 //                  on power-of-two-scaled rows: ~2^-21 relative, fp32-faithful
 //   k_hub_*        destinations with > threshold messages: chunk partials, per-hub
 //                  (max, sum), merged z rows read by the tile kernel
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "gfd_common.h"
 
 using namespace gfd;
@@ -287,11 +291,12 @@ template <int KF>
 __global__ void __launch_bounds__(1024, 8) k_fused(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, int64_t num_dst, int64_t dst_offset,
-    const int32_t* __restrict__ order, const float* __restrict__ st,
+    const int32_t* __restrict__ order, const int4* __restrict__ desc,
+    const float* __restrict__ st,
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ whi,
     const uint4* __restrict__ wlo, const float* __restrict__ bias, float slope, float dp,
     uint64_t seed, const int32_t* __restrict__ hub_rank, const float* __restrict__ zhub,
-    float* __restrict__ out, float* __restrict__ stats) {
+    float* __restrict__ out, float* __restrict__ stats, int mode) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int KH4 = 4 * Fp;                 // K of one head-half
   const int ZS = KH4 + 4;                 // padded row stride
@@ -308,9 +313,23 @@ __global__ void __launch_bounds__(1024, 8) k_fused(
   // ---- phase A: this wave's destination, all heads, in registers ----
   float z[H][KF];
   int64_t i = -1;
-  if (slot < num_dst) i = order ? order[slot] : slot;
-  if (i >= 0) {
-    const int hr = hub_rank ? hub_rank[i] : -1;
+  int4 dsc = make_int4(-1, 0, 0, -1);
+  if (slot < num_dst) {
+    if (desc) {
+      dsc = desc[slot];
+    } else {
+      const int32_t r = order ? order[slot] : int32_t(slot);
+      dsc = make_int4(r, rowptr[r], rowptr[r + 1], hub_rank ? hub_rank[r] : -1);
+    }
+    i = dsc.x;
+  }
+  if (mode == 2) {  // ablation: projection only
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+      for (int q = 0; q < KF; ++q) z[hh][q] = float(lane + hh + q) * 1e-3f;
+  } else if (i >= 0) {
+    const int hr = hub_rank ? dsc.w : -1;
     if (hr >= 0) {  // merged (normalised) by k_hub_merge
       const float* src = zhub + int64_t(hr) * (H * Fp);
 #pragma unroll
@@ -321,7 +340,7 @@ __global__ void __launch_bounds__(1024, 8) k_fused(
           z[hh][q] = f < Fp ? src[hh * Fp + f] : 0.f;
         }
     } else {
-      const int e0 = rowptr[i], e1 = rowptr[i + 1];
+      const int e0 = dsc.y, e1 = dsc.z;
       const float t_h = st[(dst_offset + i) * 16 + H + (lane & 7)];
       SegState S = aggregate_segment<KF>(x, ldx, F, col, e0, e1, st, t_h, slope, dp, seed, z);
       const float inv_lane = 1.0f / (S.ssum + kSoftmaxEps);
@@ -341,6 +360,15 @@ __global__ void __launch_bounds__(1024, 8) k_fused(
     for (int hh = 0; hh < H; ++hh)
 #pragma unroll
       for (int q = 0; q < KF; ++q) z[hh][q] = 0.f;
+  }
+  if (mode == 1) {  // ablation: aggregation only
+    float sacc = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+      for (int q = 0; q < KF; ++q) sacc += z[hh][q];
+    if (i >= 0 && lane < C) out[i * C + lane] = sacc;
+    return;
   }
   // power-of-two row scale: max |z| -> [2^13, 2^14)
   float zm = 0.f;
@@ -421,6 +449,340 @@ __global__ void __launch_bounds__(1024, 8) k_fused(
       const int r = (lane >> 4) * 4 + q;
       const int ri = rowid[r];
       if (ri >= 0) out[int64_t(ri) * C + n] = accv[q] * (rscale[r] * wu) + b;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight-stationary persistent tile kernel (one 8-wave block per CU).
+//
+//  * The projection weights never stream from L2 per tile: each wave keeps the
+//    fp16 W_hi B-fragments of its (k-step, column-tile) pairs in VGPRs for the
+//    whole launch, and W_lo of the first `nlds` k-steps sits in LDS (the rest
+//    is read from L2 just in time).
+//  * Two destinations per wave, 16 per tile.  Software pipeline per wave: while
+//    tile t's MFMA phase runs, the x rows of tile t+1's first 4 messages (and
+//    their logits) are in flight, and tile t+2's slot records are loading.
+//  * Z goes through LDS once per head-half, already split into fp16 hi/lo'
+//    (so the 4 column-tile waves do not redo the split).
+constexpr int kPWaves = 16;
+
+template <int I, int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  if constexpr (I < N) {
+    fn(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(fn);
+  }
+}
+
+struct DstPipe {  // registers of one destination in flight
+  int4 d;         // {row, e_begin, e_end, hub_rank}; row < 0 = empty slot
+  int j;          // source of message (lane >> 3) of the first batch
+};
+
+template <int KF>
+struct DstData {
+  float th;           // t_i, head lane & 7
+  float sj;           // s_j of the lane's first-batch message
+  float xv[4][KF];    // x rows of messages 0..3
+};
+
+template <int KF>
+__device__ __forceinline__ void pipe_rec(DstPipe& p, int64_t slot, int64_t num_dst,
+                                         const int4* __restrict__ desc,
+                                         const int32_t* __restrict__ cols8) {
+  const int kk = (threadIdx.x & 63) >> 3;
+  if (slot < num_dst) {
+    p.d = desc[slot];
+    p.j = cols8 ? cols8[slot * 8 + kk] : -1;
+  } else {
+    p.d = make_int4(-1, 0, 0, -1);
+    p.j = 0;
+  }
+}
+
+template <int KF>
+__device__ __forceinline__ void pipe_issue(DstPipe& p, DstData<KF>& q, const float* __restrict__ x,
+                                           int64_t ldx, int F, const int32_t* __restrict__ col,
+                                           const float* __restrict__ st, int64_t dst_offset) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  if (p.d.x < 0 || p.d.w >= 0) return;  // empty slot or hub row (merged elsewhere)
+  if (p.j < 0) p.j = col[min(p.d.y + kk, p.d.z - 1)];
+  q.th = st[(dst_offset + p.d.x) * 16 + H + h];
+  q.sj = st[int64_t(p.j) * 16 + h];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int jk = __builtin_amdgcn_readlane(p.j, 8 * k);
+    const float* xr = x + int64_t(jk) * ldx;
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) {
+      const int f = lane + 64 * qq;
+      const float t = xr[f < F ? f : F - 1];
+      q.xv[k][qq] = f < F ? t : 0.f;
+    }
+  }
+}
+
+// Aggregate one destination whose first batch is prefetched in (p, q).
+template <int KF>
+__device__ __forceinline__ void pipe_compute(const DstPipe& p, const DstData<KF>& q,
+                                             const float* __restrict__ x, int64_t ldx, int F,
+                                             int Fp, const int32_t* __restrict__ col,
+                                             const float* __restrict__ st, float slope, float dp,
+                                             uint64_t seed, const float* __restrict__ zhub,
+                                             float* __restrict__ stats, float (&z)[H][KF]) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[hh][qq] = 0.f;
+  if (p.d.x < 0) return;
+  if (p.d.w >= 0) {  // hub: merged row (already normalised)
+    const float* src = zhub + int64_t(p.d.w) * (H * Fp);
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq) {
+        const int f = lane + 64 * qq;
+        z[hh][qq] = f < Fp ? src[hh * Fp + f] : 0.f;
+      }
+    return;
+  }
+  const int e0 = p.d.y, e1 = p.d.z;
+  const float keep_scale = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+  float m = -INFINITY, l = 0.f;
+  for (int b = e0; b < e1; b += 8) {
+    const int e = b + kk;
+    const bool valid = e < e1;
+    int j;
+    float v;
+    if (b == e0) {
+      j = p.j;
+      v = leaky(q.sj + q.th, slope);
+    } else {
+      j = col[valid ? e : e1 - 1];
+      v = leaky(st[int64_t(j) * 16 + h] + q.th, slope);
+    }
+    float bm = valid ? v : -INFINITY;
+    bm = fmaxf(bm, __shfl_xor(bm, 8));
+    bm = fmaxf(bm, __shfl_xor(bm, 16));
+    bm = fmaxf(bm, __shfl_xor(bm, 32));
+    const float mn = fmaxf(m, bm);
+    const float sc = __expf(m - mn);
+    float pv = valid ? __expf(v - mn) : 0.f;
+    l = fmaf(l, sc, pv);
+    if (b != e0 && __any(sc != 1.0f)) {
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
+#pragma unroll
+        for (int qq = 0; qq < KF; ++qq) z[hh][qq] *= s;
+      }
+    }
+    m = mn;
+    if (dp > 0.f) pv = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? pv * keep_scale : 0.f;
+    const int nk = min(8, e1 - b);
+    for (int k0 = 0; k0 < nk; k0 += 4) {
+      float xl[4][KF];
+      if (b == e0 && k0 == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int qq = 0; qq < KF; ++qq) xl[k][qq] = q.xv[k][qq];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int jk = __builtin_amdgcn_readlane(j, 8 * (k0 + k));
+          const float* xr = x + int64_t(jk) * ldx;
+#pragma unroll
+          for (int qq = 0; qq < KF; ++qq) {
+            const int f = lane + 64 * qq;
+            const float t = xr[f < F ? f : F - 1];
+            xl[k][qq] = f < F ? t : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {
+          const float pk =
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), 8 * (k0 + k) + hh));
+#pragma unroll
+          for (int qq = 0; qq < KF; ++qq) z[hh][qq] = fmaf(pk, xl[k][qq], z[hh][qq]);
+        }
+    }
+  }
+  l += __shfl_xor(l, 8);
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  if (stats && lane < 8) {
+    stats[int64_t(p.d.x) * 16 + lane] = m;
+    stats[int64_t(p.d.x) * 16 + 8 + lane] = l;
+  }
+  const float inv_lane = 1.0f / (l + kSoftmaxEps);
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_lane), hh));
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[hh][qq] *= inv;
+  }
+}
+
+// power-of-two row scale so that max |z| lies in [2^13, 2^14); returns 2^-e
+template <int KF>
+__device__ __forceinline__ float scale_row(float (&z)[H][KF]) {
+  float zm = 0.f;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) zm = fmaxf(zm, fabsf(z[hh][q]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) zm = fmaxf(zm, __shfl_xor(zm, o));
+  int ex = 0;
+  if (zm > 0.f) frexpf(zm, &ex);
+  int er = 14 - ex;
+  er = er > 100 ? 100 : (er < -100 ? -100 : er);
+  const float rs = ldexpf(1.0f, er);
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) z[hh][q] *= rs;
+  return ldexpf(1.0f, -er);
+}
+
+// write all 8 heads of one row into the LDS tile as fp16 hi / lo'
+template <int KF>
+__device__ __forceinline__ void write_row(const float (&z)[H][KF], int Fp,
+                                          _Float16* __restrict__ zh, _Float16* __restrict__ zl) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) {
+      const int f = lane + 64 * q;
+      if (f < Fp) {
+        const float v = z[hh][q];
+        const _Float16 hv = (_Float16)v;
+        zh[hh * Fp + f] = hv;
+        zl[hh * Fp + f] = (_Float16)((v - (float)hv) * kLoScale);
+      }
+    }
+}
+
+// WAVES waves per block, DPW = 16 / WAVES destinations per wave (processed one
+// after the other, each written to the LDS tile right after its phase A), KQ =
+// WAVES / 4 k-step phases.  NKW: k-steps per wave (s = kq + KQ*u, u < NKW);
+// W_lo of u < U0 (s < KQ*U0) is LDS-resident, the rest is read from L2 each tile.
+template <int KF, int WAVES, int NKW, int U0>
+__global__ void __launch_bounds__(WAVES * 64, (WAVES == 16 ? 4 : 2)) k_persist(
+    const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
+    int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
+    const int32_t* __restrict__ cols8, const float* __restrict__ st,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ whi,
+    const uint4* __restrict__ wlo, const float* __restrict__ bias, float slope,
+    float dp, uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
+    float* __restrict__ stats, int64_t num_tiles) {
+  constexpr int DPW = kTile / WAVES;
+  constexpr int KQ = WAVES / 4;
+  constexpr int nlds = KQ * U0;
+  extern __shared__ __attribute__((aligned(16))) char psm[];
+  const int KP = H * Fp;            // multiple of 64
+  const int KS = KP / 32;
+  const int ZS = KP + 8;            // tile row stride in fp16 (16-B pad)
+  _Float16* Zh = reinterpret_cast<_Float16*>(psm);            // [16][ZS]
+  _Float16* Zl = Zh + kTile * ZS;                             // [16][ZS]
+  float* red = reinterpret_cast<float*>(psm + align_up(sizeof(_Float16) * 2 * kTile * ZS, 16));
+  float* rsc0 = red + (KQ - 1) * 4 * 64 * 4;                  // [2][16] by tile parity
+  int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);       // [2][16]
+  uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);     // [nlds][4][64]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = wave_uniform(tid >> 6);
+  const int ct = wave & 3, kq = wave >> 2;  // column tile, k-step phase (s = kq mod KQ)
+  const int arow = lane & 15, akg = lane >> 4;
+
+  // stationary weights: W_hi of this wave's k-steps in VGPRs, W_lo[0, nlds) in LDS
+  uint4 wh[NKW];
+#pragma unroll
+  for (int u = 0; u < NKW; ++u) {
+    const int s = kq + KQ * u;
+    wh[u] = s < KS ? whi[(s * 4 + ct) * 64 + lane] : make_uint4(0, 0, 0, 0);
+  }
+  for (int idx = tid; idx < min(nlds, KS) * 256; idx += WAVES * 64) WL[idx] = wlo[idx];
+  const float wu = hdr->w_unscale;
+  const float bcol = bias ? bias[ct * 16 + (lane & 15)] : 0.f;
+
+  DstPipe pc[DPW], pn[DPW];
+  DstData<KF> dd[DPW];
+  int64_t t = blockIdx.x;
+  const int64_t G = gridDim.x;
+#pragma unroll
+  for (int d = 0; d < DPW; ++d) {
+    pipe_rec<KF>(pc[d], t * kTile + wave * DPW + d, num_dst, desc, cols8);
+    pipe_issue<KF>(pc[d], dd[d], x, ldx, F, col, st, dst_offset);
+    pipe_rec<KF>(pn[d], (t + G) * kTile + wave * DPW + d, num_dst, desc, cols8);
+  }
+  __syncthreads();  // WL ready
+
+  for (int it = 0; t < num_tiles; t += G, ++it) {
+    float* rsc = rsc0 + (it & 1) * kTile;
+    int* rid = rid0 + (it & 1) * kTile;
+    // ---- phase A: each destination -> its fp16 hi/lo row of the Z tile ----
+#pragma unroll
+    for (int d = 0; d < DPW; ++d) {
+      const int r = wave * DPW + d;
+      float z[H][KF];
+      pipe_compute<KF>(pc[d], dd[d], x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, z);
+      const int ri = pc[d].d.x;
+      const float sr = scale_row<KF>(z);
+      write_row<KF>(z, Fp, Zh + r * ZS, Zl + r * ZS);
+      if (lane == 0) {
+        rsc[r] = sr;
+        rid[r] = ri;
+      }
+      // next tile's first batch of this destination slot goes in flight now
+      pc[d] = pn[d];
+      pipe_issue<KF>(pc[d], dd[d], x, ldx, F, col, st, dst_offset);
+      pipe_rec<KF>(pn[d], (t + 2 * G) * kTile + r, num_dst, desc, cols8);
+    }
+    __syncthreads();
+    // ---- phase B: out[16 x 64] = Z[16 x KP] . Wcat on f16 MFMA ----
+    f32x4 acc_m = {0.f, 0.f, 0.f, 0.f}, acc_x = {0.f, 0.f, 0.f, 0.f};
+    const _Float16* ah = Zh + arow * ZS + 8 * akg;
+    const _Float16* al = Zl + arow * ZS + 8 * akg;
+    static_for<0, NKW>([&](auto ui) {
+      constexpr int u = decltype(ui)::value;
+      const int s = kq + KQ * u;
+      if (s < KS) {
+        uint4 blo;
+        if constexpr (u < U0) blo = WL[(s * 4 + ct) * 64 + lane];
+        else blo = wlo[(s * 4 + ct) * 64 + lane];
+        const f16x8 a_hi = *reinterpret_cast<const f16x8*>(ah + 32 * s);
+        const f16x8 a_lo = *reinterpret_cast<const f16x8*>(al + 32 * s);
+        const f16x8 b_hi = *reinterpret_cast<const f16x8*>(&wh[u]);
+        const f16x8 b_lo = *reinterpret_cast<const f16x8*>(&blo);
+        acc_m = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_hi, acc_m, 0, 0, 0);
+        acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_lo, acc_x, 0, 0, 0);
+        acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_lo, b_hi, acc_x, 0, 0, 0);
+      }
+    });
+    f32x4 accv = acc_m + acc_x * (1.0f / kLoScale);
+    if (kq) *reinterpret_cast<f32x4*>(red + (((kq - 1) * 4 + ct) * 64 + lane) * 4) = accv;
+    __syncthreads();  // also: every MFMA of this tile is done before the next Z write
+    if (!kq) {
+#pragma unroll
+      for (int pp = 0; pp < KQ - 1; ++pp)
+        accv += *reinterpret_cast<const f32x4*>(red + ((pp * 4 + ct) * 64 + lane) * 4);
+      const int n = ct * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = (lane >> 4) * 4 + q;
+        const int ri = rid[r];
+        if (ri >= 0) out[int64_t(ri) * C + n] = accv[q] * (rsc[r] * wu) + bcol;
+      }
     }
   }
 }
@@ -552,6 +914,36 @@ gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const
   return GFD_OK;
 }
 
+// GFD_FUSED_MODE (profiling ablation only): 0 full, 1 aggregation only,
+// 2 projection only.  Outputs are wrong in modes 1 and 2.
+int fused_mode() {
+  static int m = [] {
+    const char* e = getenv("GFD_FUSED_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
+// GFD_TILE_KERNEL (A/B switch): 0 default (k_fused), 2 persistent weight-stationary.
+int tile_kernel() {
+  static int m = [] {
+    const char* e = getenv("GFD_TILE_KERNEL");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
 struct AggArgs {
   const float* x; int F; int64_t ldx;
   const int32_t* rowptr; const int32_t* col; int64_t num_dst; int64_t dst_offset;
@@ -559,6 +951,45 @@ struct AggArgs {
   gfd_plan plan; int stages; float* out; float* stats;
   float* part; float* hubstat; float* zhub;
 };
+
+constexpr size_t kLdsBytes = 160 * 1024;
+
+size_t persist_fixed_lds(int Fp, int kphases) {
+  return align_up(sizeof(_Float16) * 2 * kTile * (H * Fp + 8), 16) +
+         sizeof(float) * (kphases - 1) * 4 * 64 * 4 + sizeof(float) * 4 * kTile;
+}
+
+template <int KF>
+gfd_status launch_persist(const AggArgs& a, const PackLayout& L, int64_t tiles,
+                          hipStream_t stream) {
+  // per feature-chunk class: waves per block, k-steps per wave, LDS-resident W_lo groups
+  constexpr int WAVES = KF == 3 ? 8 : 16;
+  constexpr int KQ = WAVES / 4;
+  constexpr int NKW = (KF * 64 * H / 32 + KQ - 1) / KQ;
+  constexpr int U0 = KF == 1 ? 4 : (KF == 2 ? 5 : 8);
+  const size_t lds = persist_fixed_lds(L.Fp, KQ) + size_t(KQ * U0) * sizeof(uint4) * 256;
+  if (lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_persist<KF, WAVES, NKW, U0>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsBytes)) !=
+        hipSuccess)
+      return GFD_ERR_HIP;
+    attr_set = true;
+  }
+  int64_t grid = cu_count();
+  if (grid > tiles) grid = tiles;
+  const gfd_plan& p = a.plan;
+  const PackHeader* hdr = reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off);
+  const uint4* whi = reinterpret_cast<const uint4*>(a.packed + L.whi_off);
+  const uint4* wlo = reinterpret_cast<const uint4*>(a.packed + L.wlo_off);
+  k_persist<KF, WAVES, NKW, U0><<<int(grid), WAVES * 64, lds, stream>>>(
+      a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
+      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st, hdr, whi, wlo, a.bias,
+      a.slope, a.dp, a.seed, a.zhub, a.out, a.stats, tiles);
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
 
 template <int KF>
 gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
@@ -579,13 +1010,17 @@ gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t s
   }
   if (!(a.stages & GFD_STAGE_TILES)) return GFD_OK;
   const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
+  if constexpr (KF <= 3) {
+    if (p.slot_desc && tile_kernel() == 2) return launch_persist<KF>(a, L, tiles, stream);
+  }
   const PackHeader* hdr = reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off);
   const uint4* whi = reinterpret_cast<const uint4*>(a.packed + L.whi_off);
   const uint4* wlo = reinterpret_cast<const uint4*>(a.packed + L.wlo_off);
   k_fused<KF><<<int(tiles), kFusedWaves * 64, fused_smem(Fp), stream>>>(
-      a.x, a.F, Fp, a.ldx, a.rowptr, a.col, a.num_dst, a.dst_offset, p.row_order, a.st, hdr,
+      a.x, a.F, Fp, a.ldx, a.rowptr, a.col, a.num_dst, a.dst_offset, p.row_order,
+      reinterpret_cast<const int4*>(p.slot_desc), a.st, hdr,
       whi, wlo, a.bias, a.slope, a.dp, a.seed, p.num_hubs > 0 ? p.hub_rank : nullptr, a.zhub,
-      a.out, a.stats);
+      a.out, a.stats, fused_mode());
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
@@ -622,7 +1057,7 @@ gfd_status check_agg_args(const float* x, int64_t N, int F, int64_t ldx, const i
 gfd_plan plan_or_empty(const gfd_plan* p) {
   if (p) return *p;
   gfd_plan e;
-  e.row_order = e.hub_rank = e.hub_chunk = e.hub_chunk_ptr = e.hub_dst = nullptr;
+  e.row_order = e.slot_desc = e.slot_cols = e.hub_rank = e.hub_chunk = e.hub_chunk_ptr = e.hub_dst = nullptr;
   e.num_hubs = e.num_chunks = 0;
   return e;
 }

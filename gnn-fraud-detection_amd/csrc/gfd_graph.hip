@@ -148,9 +148,39 @@ __global__ void k_order_keys(const int32_t* __restrict__ rowptr, int64_t n, int3
   }
 }
 
+// slot -> {row, e_begin, e_end, hub_rank} and the row's first 8 sources
+// (clamped to the last one): one 16-B + one 32-B load replace the
+// order -> hub_rank -> rowptr -> col chain of dependent loads in the tile kernel.
+__global__ void k_slot_desc(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                            int64_t n, const int32_t* __restrict__ order,
+                            const int32_t* __restrict__ hub_rank, int4* __restrict__ desc,
+                            int32_t* __restrict__ cols8) {
+  for (int64_t s = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; s < n;
+       s += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t i = order ? order[s] : int32_t(s);
+    const int32_t b = rowptr[i], e = rowptr[i + 1];
+    desc[s] = make_int4(i, b, e, hub_rank ? hub_rank[i] : -1);
+    if (cols8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cols8[s * 8 + k] = col[min(b + k, e - 1)];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t n,
+                         const int32_t* order, const int32_t* hub_rank, int32_t* desc,
+                         int32_t* slot_cols, gfd_stream_t stream_) {
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (n <= 0 || !rowptr || !desc || (slot_cols && !col)) return GFD_ERR_ARGUMENT;
+  k_slot_desc<<<grid_for(n), kBlock, 0, stream>>>(rowptr, col, n, order, hub_rank,
+                                                  reinterpret_cast<int4*>(desc), slot_cols);
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
 
 const char* gfd_status_string(gfd_status s) {
   switch (s) {

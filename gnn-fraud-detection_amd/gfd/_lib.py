@@ -21,7 +21,7 @@ P = ct.c_void_p
 
 class GfdPlan(ct.Structure):
     """``gfd_plan`` (include/gfd.h)."""
-    _fields_ = [("row_order", P), ("hub_rank", P), ("hub_chunk", P), ("hub_chunk_ptr", P),
+    _fields_ = [("row_order", P), ("slot_desc", P), ("slot_cols", P), ("hub_rank", P), ("hub_chunk", P), ("hub_chunk_ptr", P),
                 ("hub_dst", P), ("num_hubs", c_i64), ("num_chunks", c_i64)]
 
 
@@ -40,6 +40,7 @@ SIGNATURES = {
                               ct.POINTER(c_i64), ct.POINTER(c_i64), P, c_sz, P]),
     "gfd_order_workspace_size": (c_sz, [c_i64, c_i32]),
     "gfd_plan_order": (c_i32, [P, c_i64, c_i32, P, P, c_sz, P]),
+    "gfd_plan_desc": (c_i32, [P, P, c_i64, P, P, P, P, P]),
     "gfd_gat_packed_size": (c_sz, [ct.c_int, ct.c_int, ct.c_int]),
     "gfd_gat_pack_weights": (c_i32, [P, P, P, ct.c_int, ct.c_int, ct.c_int, P, P]),
     "gfd_gat_logits": (c_i32, [P, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),

@@ -35,6 +35,8 @@ class Plan:
     (destinations by descending message count) and the hub split."""
     num_dst: int
     row_order: Optional[torch.Tensor]
+    slot_desc: Optional[torch.Tensor]
+    slot_cols: Optional[torch.Tensor]
     hub_rank: Optional[torch.Tensor]
     hub_chunk: Optional[torch.Tensor]
     hub_chunk_ptr: Optional[torch.Tensor]
@@ -48,7 +50,8 @@ class Plan:
         if self._c is None:
             p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
             hubs = self.num_hubs > 0
-            self._c = _lib.GfdPlan(p(self.row_order), p(self.hub_rank) if hubs else None,
+            self._c = _lib.GfdPlan(p(self.row_order), p(self.slot_desc), p(self.slot_cols),
+                                   p(self.hub_rank) if hubs else None,
                                    p(self.hub_chunk) if hubs else None,
                                    p(self.hub_chunk_ptr) if hubs else None,
                                    p(self.hub_dst) if hubs else None, self.num_hubs,
@@ -63,8 +66,10 @@ class Plan:
 
 
 def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
-               chunk: int = HUB_CHUNK, order: bool = True) -> Plan:
-    """Plan for the destination range described by ``rowptr`` ([n+1] int32)."""
+               chunk: int = HUB_CHUNK, order: bool = True,
+               col: Optional[torch.Tensor] = None) -> Plan:
+    """Plan for the destination range described by ``rowptr`` ([n+1] int32,
+    absolute positions into ``col``)."""
     n = rowptr.numel() - 1
     dev = rowptr.device
     lib = _lib.load()
@@ -86,14 +91,22 @@ def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THR
         ws = _ws(lib.gfd_order_workspace_size(n, threshold), dev)
         _lib.call("gfd_plan_order", rowptr.data_ptr(), n, threshold, row_order.data_ptr(),
                   ws.data_ptr(), ws.numel(), stream)
-    return Plan(n, row_order, hub_rank, hub_chunk[:4 * nc.value], hub_chunk_ptr[:nh.value + 1],
-                hub_dst[:nh.value], nh.value, nc.value)
+    slot_desc = slot_cols = None
+    if n > 0:
+        slot_desc = torch.empty(4 * n, dtype=torch.int32, device=dev)
+        if col is not None:
+            slot_cols = torch.empty(8 * n, dtype=torch.int32, device=dev)
+        _lib.call("gfd_plan_desc", rowptr.data_ptr(), _lib.ptr(col), n, _lib.ptr(row_order),
+                  hub_rank.data_ptr() if nh.value > 0 else None, slot_desc.data_ptr(),
+                  _lib.ptr(slot_cols), stream)
+    return Plan(n, row_order, slot_desc, slot_cols, hub_rank, hub_chunk[:4 * nc.value],
+                hub_chunk_ptr[:nh.value + 1], hub_dst[:nh.value], nh.value, nc.value)
 
 
 # backwards-compatible name
 def plan_hubs(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
               chunk: int = HUB_CHUNK) -> Plan:
-    return build_plan(rowptr, num_messages, threshold, chunk)
+    return build_plan(rowptr, num_messages, threshold, chunk)  # no slot_cols
 
 
 @dataclass
@@ -120,7 +133,7 @@ class CSRGraph:
 
     def plan(self) -> Plan:
         if self._plan is None:
-            self._plan = build_plan(self.rowptr, self.num_messages)
+            self._plan = build_plan(self.rowptr, self.num_messages, col=self.col)
         return self._plan
 
     def csc(self) -> CSC:
@@ -140,7 +153,7 @@ class CSRGraph:
         """Destination range [lo, hi): a rowptr view (absolute positions into col)."""
         rp = self.rowptr[lo:hi + 1]
         m = int(self.rowptr[hi].item()) - int(self.rowptr[lo].item())
-        return CSRShard(self, lo, hi, rp, m, build_plan(rp, m))
+        return CSRShard(self, lo, hi, rp, m, build_plan(rp, m, col=self.col))
 
 
 @dataclass

@@ -96,6 +96,14 @@ size_t gfd_order_workspace_size(int64_t num_dst, int32_t cap);
 gfd_status gfd_plan_order(const int32_t* rowptr, int64_t num_dst, int32_t cap, int32_t* order,
                           void* ws, size_t ws_bytes, gfd_stream_t stream);
 
+/* Slot descriptors: desc[4*s .. 4*s+3] = {row, e_begin, e_end, hub_rank} of
+ * tile slot s (row = order[s], or s when order is NULL; hub_rank -1 when
+ * NULL) and, when slot_cols is not NULL, slot_cols[8*s + k] = col[min(e_begin
+ * + k, e_end - 1)] (the first 8 sources, prefetched one tile ahead). */
+gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t num_dst,
+                         const int32_t* order, const int32_t* hub_rank, int32_t* desc,
+                         int32_t* slot_cols, gfd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * GATConv forward (PyG GATConv.forward, concat=False, add_self_loops=True,
  * bias=True; gat.py:80 / tgn.py:94):
@@ -126,6 +134,8 @@ gfd_status gfd_gat_logits(const float* x, int64_t num_rows, int in_features, int
  * gfd_plan_hubs on the range's rowptr. */
 typedef struct gfd_plan {
   const int32_t* row_order;     /* [num_dst] tile order, or NULL for 0..num_dst-1      */
+  const int32_t* slot_desc;     /* [4*num_dst] gfd_plan_desc output, or NULL           */
+  const int32_t* slot_cols;     /* [8*num_dst] gfd_plan_desc output, or NULL           */
   const int32_t* hub_rank;      /* [num_dst] -1 or hub index (NULL iff num_hubs == 0)  */
   const int32_t* hub_chunk;     /* [4*num_chunks] {hub, e_begin, e_end, dst}           */
   const int32_t* hub_chunk_ptr; /* [num_hubs + 1]                                      */
