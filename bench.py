@@ -143,13 +143,13 @@ def main():
     a_d = glorot((1, H, C), gen, dev).contiguous()
     bias = torch.zeros(C, device=dev)
 
-    lo, hi = gdist.shard_ranges(g.rowptr, rank, world) if world > 1 else (0, N)
+    spec = gdist.ShardSpec(g.rowptr, rank, world)   # dst shard + logits node block
+    lo, hi = spec.dst_lo, spec.dst_hi
     shard = g.shard(lo, hi)
     plan = shard.plan
     n_dst = hi - lo
     m_local = int(shard.rowptr[-1].item()) - int(shard.rowptr[0].item())
-    nb = gdist.node_bounds(N, world)
-    st_lo, st_hi = nb[rank], nb[rank + 1]
+    st_lo, st_hi = spec.node_lo, spec.node_hi
 
     packed = torch.empty(lib.gfd_gat_packed_size(F, H, C), dtype=torch.uint8, device=dev)
     st = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)

@@ -282,13 +282,26 @@ __device__ __forceinline__ void mfma_step(const float* __restrict__ Zrow, const 
   acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bhi, acc_x, 0, 0, 0);
 }
 
+// same with the A fragment already split (fp16 hi / lo' rows in LDS)
+__device__ __forceinline__ void mfma_step_split(const _Float16* __restrict__ zh,
+                                                const _Float16* __restrict__ zl, const uint4& bh,
+                                                const uint4& bl, f32x4& acc_m, f32x4& acc_x) {
+  const f16x8 ahi = *reinterpret_cast<const f16x8*>(zh);
+  const f16x8 alo = *reinterpret_cast<const f16x8*>(zl);
+  const f16x8 bhi = *reinterpret_cast<const f16x8*>(&bh);
+  const f16x8 blo = *reinterpret_cast<const f16x8*>(&bl);
+  acc_m = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bhi, acc_m, 0, 0, 0);
+  acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc_x, 0, 0, 0);
+  acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bhi, acc_x, 0, 0, 0);
+}
+
 // ---------------------------------------------------------------------------
 // Fused tile kernel: 16 destinations per block, one per wave.  The Z tile goes
 // through LDS one head-half at a time (16 x 4Fp fp32 = 43 KB at F = 166, two
 // blocks per CU).  MFMA work split: column tile ct = w & 3, k-step phase kq = w >> 2;
 // the four k-phase partials are summed through LDS at the end.
-template <int KF>
-__global__ void __launch_bounds__(1024, 8) k_fused(
+template <int KF, int OCC>
+__global__ void __launch_bounds__(1024, OCC) k_fused(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, int64_t num_dst, int64_t dst_offset,
     const int32_t* __restrict__ order, const int4* __restrict__ desc,
@@ -299,11 +312,13 @@ __global__ void __launch_bounds__(1024, 8) k_fused(
     float* __restrict__ out, float* __restrict__ stats, int mode) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int KH4 = 4 * Fp;                 // K of one head-half
-  const int ZS = KH4 + 4;                 // padded row stride
+  const int ZS = KH4 + 8;                 // padded row stride (fp16 elements, 16 B pad)
   const int KH = KH4 / 32;                // k-steps per half
-  float* Z = smem;                        // [16][ZS]
-  float* red = Z + kTile * ZS;            // [3][4][64][4] k-phase partials (x2: main, cross)
-  float* rscale = red + 2 * 3 * 4 * 64 * 4;   // [16] per-row 2^-e
+  // the half-tile is stored already split: fp16 hi and lo' = (v - hi) * 2^11
+  _Float16* Zh = reinterpret_cast<_Float16*>(smem);   // [16][ZS]
+  _Float16* Zl = Zh + kTile * ZS;                     // [16][ZS]
+  float* red = smem + kTile * ZS;         // [3][4][64][4] k-phase partials
+  float* rscale = red + 3 * 4 * 64 * 4;   // [16] per-row 2^-e
   int* rowid = reinterpret_cast<int*>(rscale + kTile);  // [16]
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
@@ -395,7 +410,8 @@ __global__ void __launch_bounds__(1024, 8) k_fused(
   // ---- phase B over two head-halves ----
   const int arow = lane & 15, akg = lane >> 4;
   f32x4 acc_m = {0.f, 0.f, 0.f, 0.f}, acc_x = {0.f, 0.f, 0.f, 0.f};
-  float* zr = Z + wave * ZS;
+  _Float16* zrh = Zh + wave * ZS;
+  _Float16* zrl = Zl + wave * ZS;
 #pragma unroll
   for (int hg = 0; hg < 2; ++hg) {
     // W fragments of this wave's first two k-steps: in flight across the barrier
@@ -415,18 +431,24 @@ __global__ void __launch_bounds__(1024, 8) k_fused(
 #pragma unroll
       for (int q = 0; q < KF; ++q) {
         const int f = lane + 64 * q;
-        if (f < Fp) zr[hh * Fp + f] = z[4 * hg + hh][q];
+        if (f < Fp) {
+          const float v = z[4 * hg + hh][q];
+          const _Float16 hv = (_Float16)v;
+          zrh[hh * Fp + f] = hv;
+          zrl[hh * Fp + f] = (_Float16)((v - (float)hv) * kLoScale);
+        }
       }
     __syncthreads();
-    const float* zb = Z + arow * ZS + 8 * akg;
+    const _Float16* zbh = Zh + arow * ZS + 8 * akg;
+    const _Float16* zbl = Zl + arow * ZS + 8 * akg;
     for (int s = kq; s < KH; s += 8) {
-      mfma_step(zb + 32 * s, bh0, bl0, acc_m, acc_x);
+      mfma_step_split(zbh + 32 * s, zbl + 32 * s, bh0, bl0, acc_m, acc_x);
       if (s + 8 < KH) {
         bh0 = whi[((gs0 + s + 8) * 4 + ct) * 64 + lane];
         bl0 = wlo[((gs0 + s + 8) * 4 + ct) * 64 + lane];
       }
       if (s + 4 < KH) {
-        mfma_step(zb + 32 * (s + 4), bh1, bl1, acc_m, acc_x);
+        mfma_step_split(zbh + 32 * (s + 4), zbl + 32 * (s + 4), bh1, bl1, acc_m, acc_x);
         if (s + 12 < KH) {
           bh1 = whi[((gs0 + s + 12) * 4 + ct) * 64 + lane];
           bl1 = wlo[((gs0 + s + 12) * 4 + ct) * 64 + lane];
@@ -894,8 +916,8 @@ __global__ void __launch_bounds__(256) k_hub_merge(const float* __restrict__ par
 // ---------------------------------------------------------------------------
 inline int kf_for(int F) { return (F + 63) / 64; }
 
-size_t fused_smem(int Fp) {
-  return sizeof(float) * (kTile * (4 * Fp + 4) + 2 * 3 * 4 * 64 * 4 + 2 * kTile);
+size_t fused_smem(int Fp) {  // fp16 hi + lo half-tile (= 4 B per element) + partials + rows
+  return sizeof(float) * (kTile * (4 * Fp + 8) + 3 * 4 * 64 * 4 + 2 * kTile);
 }
 
 gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const float* uv, int Fu,
@@ -916,6 +938,18 @@ gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const
 
 // GFD_FUSED_MODE (profiling ablation only): 0 full, 1 aggregation only,
 // 2 projection only.  Outputs are wrong in modes 1 and 2.
+// Waves per SIMD the tile kernel is compiled for.  KF <= 2 fits 64 VGPRs (8 waves
+// per SIMD, two blocks per CU); KF = 3 at 64 VGPRs spills ~52 B/lane per
+// destination (33 GB of scratch writes at C4), so it runs at 4 waves per SIMD.
+// GFD_FUSED_OCC=4|8 overrides (A/B experiments).
+int fused_occ(int KF) {
+  static int m = [] {
+    const char* e = getenv("GFD_FUSED_OCC");
+    return e ? atoi(e) : 0;
+  }();
+  return m ? m : (KF >= 3 ? 4 : 8);
+}
+
 int fused_mode() {
   static int m = [] {
     const char* e = getenv("GFD_FUSED_MODE");
@@ -1016,7 +1050,8 @@ gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t s
   const PackHeader* hdr = reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off);
   const uint4* whi = reinterpret_cast<const uint4*>(a.packed + L.whi_off);
   const uint4* wlo = reinterpret_cast<const uint4*>(a.packed + L.wlo_off);
-  k_fused<KF><<<int(tiles), kFusedWaves * 64, fused_smem(Fp), stream>>>(
+  auto kern = fused_occ(KF) == 4 ? &k_fused<KF, 4> : &k_fused<KF, 8>;
+  kern<<<int(tiles), kFusedWaves * 64, fused_smem(Fp), stream>>>(
       a.x, a.F, Fp, a.ldx, a.rowptr, a.col, a.num_dst, a.dst_offset, p.row_order,
       reinterpret_cast<const int4*>(p.slot_desc), a.st, hdr,
       whi, wlo, a.bias, a.slope, a.dp, a.seed, p.num_hubs > 0 ? p.hub_rank : nullptr, a.zhub,

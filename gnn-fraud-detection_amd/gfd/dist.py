@@ -17,7 +17,7 @@ output instead.
 """
 from __future__ import annotations
 
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -59,3 +59,121 @@ def all_gather_rows(local: torch.Tensor, n: int, parts: int, group=None) -> torc
 def shard_ranges(rowptr: torch.Tensor, rank: int, world: int) -> Tuple[int, int]:
     b = edge_balanced_bounds(rowptr, world)
     return b[rank], b[rank + 1]
+
+
+class ShardSpec:
+    """One rank's share of a destination-sharded layer.
+
+    ``dst_lo:dst_hi`` -- the destinations (and so the CSR messages) this rank
+    owns, balanced by message count; ``node_lo:node_hi`` -- the equal node
+    block whose attention logits this rank computes before the all-gather.
+    """
+
+    def __init__(self, rowptr: torch.Tensor, rank: int, world: int):
+        n = rowptr.numel() - 1
+        self.rank, self.world, self.num_nodes = rank, world, n
+        self.dst_bounds = edge_balanced_bounds(rowptr, world)
+        self.node_bounds = node_bounds(n, world)
+        self.dst_lo, self.dst_hi = self.dst_bounds[rank], self.dst_bounds[rank + 1]
+        self.node_lo, self.node_hi = self.node_bounds[rank], self.node_bounds[rank + 1]
+
+    def __repr__(self) -> str:
+        return (f"ShardSpec(rank={self.rank}/{self.world}, dst=[{self.dst_lo},{self.dst_hi}), "
+                f"nodes=[{self.node_lo},{self.node_hi}))")
+
+
+def all_gather_v_rows(local: torch.Tensor, bounds: List[int], group=None) -> torch.Tensor:
+    """All-gather uneven row blocks (``bounds[r]:bounds[r+1]`` from rank r).
+
+    RCCL's all-gather wants equal blocks, so each block is zero-padded to the
+    largest one, gathered in one collective and the padding dropped."""
+    import torch.distributed as dist
+    world = len(bounds) - 1
+    sizes = [bounds[r + 1] - bounds[r] for r in range(world)]
+    per = max(max(sizes), 1)
+    cols = local.size(1)
+    buf = local.new_zeros((per, cols))
+    if local.size(0):
+        buf[:local.size(0)] = local
+    out = local.new_empty((per * world, cols))
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return torch.cat([out[r * per:r * per + sizes[r]] for r in range(world)])
+
+
+def pack_weights(weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor) -> torch.Tensor:
+    """fp16 hi/lo MFMA fragments + folded attention vectors (gfd_gat_pack_weights)."""
+    from . import _lib
+    from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
+    lib = _lib.load()
+    H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
+    F = weight.size(1)
+    if weight.shape != (H * C, F):
+        raise ValueError(f"weight must be [{H * C}, F], got {tuple(weight.shape)}")
+    dev = weight.device
+    packed = torch.empty(lib.gfd_gat_packed_size(F, H, C), dtype=torch.uint8, device=dev)
+    _lib.call("gfd_gat_pack_weights", weight.contiguous().data_ptr(),
+              att_src.contiguous().data_ptr(), att_dst.contiguous().data_ptr(), F, H, C,
+              packed.data_ptr(), _lib.stream_handle(dev))
+    return packed
+
+
+def shard_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec) -> torch.Tensor:
+    """``[node_hi - node_lo, 16]`` attention logits (s | t) of this rank's node block."""
+    from . import _lib
+    from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
+    H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
+    rows = spec.node_hi - spec.node_lo
+    st_local = torch.empty((rows, 2 * H), dtype=torch.float32, device=x.device)
+    if rows > 0:
+        _lib.call("gfd_gat_logits", x[spec.node_lo:].data_ptr(), rows, x.size(1), x.stride(0),
+                  packed.data_ptr(), H, C, st_local.data_ptr(), _lib.stream_handle(x.device))
+    return st_local
+
+
+def shard_aggregate(x: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tensor,
+                    bias: Optional[torch.Tensor], spec: ShardSpec,
+                    negative_slope: float = 0.2) -> torch.Tensor:
+    """``[dst_hi - dst_lo, 64]`` outputs of this rank's destinations, given the
+    all-gathered ``[N, 16]`` logits (gfd_gat_aggregate, hubs + tiles)."""
+    from . import _lib
+    from .graph import _ws
+    from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
+    lib = _lib.load()
+    H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
+    N, F = x.shape
+    n_dst = spec.dst_hi - spec.dst_lo
+    out = torch.empty((n_dst, C), dtype=torch.float32, device=x.device)
+    if n_dst == 0:
+        return out
+    shard = graph.shard(spec.dst_lo, spec.dst_hi)
+    plan = shard.plan
+    ws = _ws(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, plan.num_hubs, plan.num_chunks),
+             x.device)
+    _lib.call("gfd_gat_aggregate", x.data_ptr(), N, F, x.stride(0), shard.rowptr.data_ptr(),
+              graph.col.data_ptr(), n_dst, spec.dst_lo, st.data_ptr(), packed.data_ptr(),
+              _lib.ptr(bias), H, C, float(negative_slope), 0.0, 0, plan.cstruct(),
+              3, out.data_ptr(), None, ws.data_ptr(), ws.numel(), _lib.stream_handle(x.device))
+    return out
+
+
+def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torch.Tensor,
+                     att_dst: torch.Tensor, bias: Optional[torch.Tensor], spec: ShardSpec,
+                     negative_slope: float = 0.2, gather_output: bool = True,
+                     group=None) -> torch.Tensor:
+    """Destination-sharded GATConv forward (eval) on this rank's GPU.
+
+    ``x`` is halo-resident (all N rows on every rank, row stride may be
+    padded), ``graph`` the full CSR.  Steps: pack weights -> logits of the
+    rank's node block -> RCCL all-gather of the ``[N, 16]`` logits -> fused
+    aggregate-project over the rank's destinations -> (optionally)
+    all-gather-v of the ``[n_dst, 64]`` outputs.
+    """
+    if x.stride(1) != 1:
+        raise ValueError("x rows must be contiguous")
+    packed = pack_weights(weight, att_src, att_dst)
+    st_local = shard_logits(x, packed, spec)
+    st = all_gather_rows(st_local, x.size(0), spec.world, group=group)
+    out = shard_aggregate(x, graph, st, packed, bias, spec, negative_slope)
+    if gather_output:
+        return all_gather_v_rows(out, spec.dst_bounds, group=group)
+    return out
