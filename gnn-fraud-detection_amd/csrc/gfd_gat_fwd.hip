@@ -190,7 +190,7 @@ template <int KF>
 __device__ __forceinline__ SegState aggregate_segment(
     const float* __restrict__ x, int64_t ldx, int F, const int32_t* __restrict__ col, int e0,
     int e1, const float* __restrict__ st, float t_h, float slope, float dp, uint64_t seed,
-    float (&acc)[H][KF]) {
+    float (&acc)[H][KF], int j_first = -1) {
   const int lane = threadIdx.x & 63;
   const int h = lane & 7, kk = lane >> 3;
   const float keep_scale = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
@@ -202,7 +202,8 @@ __device__ __forceinline__ SegState aggregate_segment(
   for (int b = e0; b < e1; b += 8) {
     const int e = b + kk;
     const bool valid = e < e1;
-    const int j = col[valid ? e : e1 - 1];  // clamped: every load is in bounds
+    // clamped: every load is in bounds; the first batch may come prefetched
+    const int j = (b == e0 && j_first >= 0) ? j_first : col[valid ? e : e1 - 1];
     const float v = leaky(st[int64_t(j) * 16 + h] + t_h, slope);
     float bm = valid ? v : -INFINITY;
     bm = fmaxf(bm, __shfl_xor(bm, 8));
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, int64_t num_dst, int64_t dst_offset,
     const int32_t* __restrict__ order, const int4* __restrict__ desc,
-    const float* __restrict__ st,
+    const int32_t* __restrict__ cols8, const float* __restrict__ st,
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ whi,
     const uint4* __restrict__ wlo, const float* __restrict__ bias, float slope, float dp,
     uint64_t seed, const int32_t* __restrict__ hub_rank, const float* __restrict__ zhub,
@@ -329,8 +330,11 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
   float z[H][KF];
   int64_t i = -1;
   int4 dsc = make_int4(-1, 0, 0, -1);
+  int j_first = -1;
   if (slot < num_dst) {
     if (desc) {
+      // the slot record and its first 8 sources load together: one round trip
+      if (cols8) j_first = cols8[slot * 8 + ((threadIdx.x & 63) >> 3)];
       dsc = desc[slot];
     } else {
       const int32_t r = order ? order[slot] : int32_t(slot);
@@ -357,7 +361,8 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
     } else {
       const int e0 = dsc.y, e1 = dsc.z;
       const float t_h = st[(dst_offset + i) * 16 + H + (lane & 7)];
-      SegState S = aggregate_segment<KF>(x, ldx, F, col, e0, e1, st, t_h, slope, dp, seed, z);
+      SegState S =
+          aggregate_segment<KF>(x, ldx, F, col, e0, e1, st, t_h, slope, dp, seed, z, j_first);
       const float inv_lane = 1.0f / (S.ssum + kSoftmaxEps);
       if (stats && lane < 8) {
         stats[i * 16 + lane] = S.m;
@@ -408,20 +413,25 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
   }
 
   // ---- phase B over two head-halves ----
+  // (addresses below derive from an opaque copy of Fp so that the compiler does
+  // not compute them before phase A and hold them through it)
+  int Fq = Fp;
+  asm volatile("" : "+s"(Fq));
+  const int ZSq = 4 * Fq + 8, KHq = Fq / 8;
   const int arow = lane & 15, akg = lane >> 4;
   f32x4 acc_m = {0.f, 0.f, 0.f, 0.f}, acc_x = {0.f, 0.f, 0.f, 0.f};
-  _Float16* zrh = Zh + wave * ZS;
-  _Float16* zrl = Zl + wave * ZS;
+  _Float16* zrh = Zh + wave * ZSq;
+  _Float16* zrl = Zl + wave * ZSq;
 #pragma unroll
   for (int hg = 0; hg < 2; ++hg) {
     // W fragments of this wave's first two k-steps: in flight across the barrier
-    const int gs0 = hg * KH;
+    const int gs0 = hg * KHq;
     uint4 bh0 = {0, 0, 0, 0}, bl0 = {0, 0, 0, 0}, bh1 = {0, 0, 0, 0}, bl1 = {0, 0, 0, 0};
-    if (kq < KH) {
+    if (kq < KHq) {
       bh0 = whi[((gs0 + kq) * 4 + ct) * 64 + lane];
       bl0 = wlo[((gs0 + kq) * 4 + ct) * 64 + lane];
     }
-    if (kq + 4 < KH) {
+    if (kq + 4 < KHq) {
       bh1 = whi[((gs0 + kq + 4) * 4 + ct) * 64 + lane];
       bl1 = wlo[((gs0 + kq + 4) * 4 + ct) * 64 + lane];
     }
@@ -431,25 +441,25 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
 #pragma unroll
       for (int q = 0; q < KF; ++q) {
         const int f = lane + 64 * q;
-        if (f < Fp) {
+        if (f < Fq) {
           const float v = z[4 * hg + hh][q];
           const _Float16 hv = (_Float16)v;
-          zrh[hh * Fp + f] = hv;
-          zrl[hh * Fp + f] = (_Float16)((v - (float)hv) * kLoScale);
+          zrh[hh * Fq + f] = hv;
+          zrl[hh * Fq + f] = (_Float16)((v - (float)hv) * kLoScale);
         }
       }
     __syncthreads();
-    const _Float16* zbh = Zh + arow * ZS + 8 * akg;
-    const _Float16* zbl = Zl + arow * ZS + 8 * akg;
-    for (int s = kq; s < KH; s += 8) {
+    const _Float16* zbh = Zh + arow * ZSq + 8 * akg;
+    const _Float16* zbl = Zl + arow * ZSq + 8 * akg;
+    for (int s = kq; s < KHq; s += 8) {
       mfma_step_split(zbh + 32 * s, zbl + 32 * s, bh0, bl0, acc_m, acc_x);
-      if (s + 8 < KH) {
+      if (s + 8 < KHq) {
         bh0 = whi[((gs0 + s + 8) * 4 + ct) * 64 + lane];
         bl0 = wlo[((gs0 + s + 8) * 4 + ct) * 64 + lane];
       }
-      if (s + 4 < KH) {
+      if (s + 4 < KHq) {
         mfma_step_split(zbh + 32 * (s + 4), zbl + 32 * (s + 4), bh1, bl1, acc_m, acc_x);
-        if (s + 12 < KH) {
+        if (s + 12 < KHq) {
           bh1 = whi[((gs0 + s + 12) * 4 + ct) * 64 + lane];
           bl1 = wlo[((gs0 + s + 12) * 4 + ct) * 64 + lane];
         }
@@ -675,18 +685,18 @@ __device__ __forceinline__ float scale_row(float (&z)[H][KF]) {
   return ldexpf(1.0f, -er);
 }
 
-// write all 8 heads of one row into the LDS tile as fp16 hi / lo'
+// write heads [4*hg, 4*hg+4) of one row into the half-tile as fp16 hi / lo'
 template <int KF>
-__device__ __forceinline__ void write_row(const float (&z)[H][KF], int Fp,
-                                          _Float16* __restrict__ zh, _Float16* __restrict__ zl) {
+__device__ __forceinline__ void write_half(const float (&z)[H][KF], int hg, int Fp,
+                                           _Float16* __restrict__ zh, _Float16* __restrict__ zl) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int hh = 0; hh < H; ++hh)
+  for (int hh = 0; hh < 4; ++hh)
 #pragma unroll
     for (int q = 0; q < KF; ++q) {
       const int f = lane + 64 * q;
       if (f < Fp) {
-        const float v = z[hh][q];
+        const float v = z[4 * hg + hh][q];
         const _Float16 hv = (_Float16)v;
         zh[hh * Fp + f] = hv;
         zl[hh * Fp + f] = (_Float16)((v - (float)hv) * kLoScale);
@@ -694,117 +704,570 @@ __device__ __forceinline__ void write_row(const float (&z)[H][KF], int Fp,
     }
 }
 
-// WAVES waves per block, DPW = 16 / WAVES destinations per wave (processed one
-// after the other, each written to the LDS tile right after its phase A), KQ =
-// WAVES / 4 k-step phases.  NKW: k-steps per wave (s = kq + KQ*u, u < NKW);
-// W_lo of u < U0 (s < KQ*U0) is LDS-resident, the rest is read from L2 each tile.
-template <int KF, int WAVES, int NKW, int U0>
-__global__ void __launch_bounds__(WAVES * 64, (WAVES == 16 ? 4 : 2)) k_persist(
+// 16 waves, one destination per wave and tile; wave (ct = w & 3, kq = w >> 2)
+// owns the MFMA k-steps s = kq + 4u (u < NKW) of column tile ct: their W_hi
+// fragments live in VGPRs for the whole launch, W_lo of k-steps s < nl in LDS,
+// the rest of W_lo streams from L2 (nl is as large as the LDS allows).
+template <int KF, int NKW>
+__global__ void __launch_bounds__(kPWaves * 64, 4) k_persist(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
     const int32_t* __restrict__ cols8, const float* __restrict__ st,
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ whi,
-    const uint4* __restrict__ wlo, const float* __restrict__ bias, float slope,
+    const uint4* __restrict__ wlo, int nl, const float* __restrict__ bias, float slope,
     float dp, uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
     float* __restrict__ stats, int64_t num_tiles) {
-  constexpr int DPW = kTile / WAVES;
-  constexpr int KQ = WAVES / 4;
-  constexpr int nlds = KQ * U0;
   extern __shared__ __attribute__((aligned(16))) char psm[];
-  const int KP = H * Fp;            // multiple of 64
-  const int KS = KP / 32;
-  const int ZS = KP + 8;            // tile row stride in fp16 (16-B pad)
+  const int KH4 = 4 * Fp;           // K of a head-half (multiple of 32)
+  const int KH = KH4 / 32;          // k-steps per half
+  const int KS = 2 * KH;
+  const int ZS = KH4 + 8;           // half-tile row stride in fp16 (16-B pad)
   _Float16* Zh = reinterpret_cast<_Float16*>(psm);            // [16][ZS]
   _Float16* Zl = Zh + kTile * ZS;                             // [16][ZS]
-  float* red = reinterpret_cast<float*>(psm + align_up(sizeof(_Float16) * 2 * kTile * ZS, 16));
-  float* rsc0 = red + (KQ - 1) * 4 * 64 * 4;                  // [2][16] by tile parity
+  float* red = reinterpret_cast<float*>(Zl + kTile * ZS);     // [3][4][64][4]
+  float* rsc0 = red + 3 * 4 * 64 * 4;                         // [2][16] by tile parity
   int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);       // [2][16]
-  uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);     // [nlds][4][64]
+  uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);     // [nl][4][64]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = wave_uniform(tid >> 6);
-  const int ct = wave & 3, kq = wave >> 2;  // column tile, k-step phase (s = kq mod KQ)
+  const int ct = wave & 3, kq = wave >> 2;
   const int arow = lane & 15, akg = lane >> 4;
 
-  // stationary weights: W_hi of this wave's k-steps in VGPRs, W_lo[0, nlds) in LDS
   uint4 wh[NKW];
 #pragma unroll
   for (int u = 0; u < NKW; ++u) {
-    const int s = kq + KQ * u;
+    const int s = kq + 4 * u;
     wh[u] = s < KS ? whi[(s * 4 + ct) * 64 + lane] : make_uint4(0, 0, 0, 0);
   }
-  for (int idx = tid; idx < min(nlds, KS) * 256; idx += WAVES * 64) WL[idx] = wlo[idx];
+  for (int idx = tid; idx < nl * 256; idx += kPWaves * 64) WL[idx] = wlo[idx];
   const float wu = hdr->w_unscale;
   const float bcol = bias ? bias[ct * 16 + (lane & 15)] : 0.f;
 
-  DstPipe pc[DPW], pn[DPW];
-  DstData<KF> dd[DPW];
+  DstPipe pc, pn;
+  DstData<KF> dd;
   int64_t t = blockIdx.x;
   const int64_t G = gridDim.x;
-#pragma unroll
-  for (int d = 0; d < DPW; ++d) {
-    pipe_rec<KF>(pc[d], t * kTile + wave * DPW + d, num_dst, desc, cols8);
-    pipe_issue<KF>(pc[d], dd[d], x, ldx, F, col, st, dst_offset);
-    pipe_rec<KF>(pn[d], (t + G) * kTile + wave * DPW + d, num_dst, desc, cols8);
-  }
+  pipe_rec<KF>(pc, t * kTile + wave, num_dst, desc, cols8);
+  pipe_issue<KF>(pc, dd, x, ldx, F, col, st, dst_offset);
+  pipe_rec<KF>(pn, (t + G) * kTile + wave, num_dst, desc, cols8);
   __syncthreads();  // WL ready
 
   for (int it = 0; t < num_tiles; t += G, ++it) {
+    // An opaque per-tile copy of the row width: every address derived from it is
+    // recomputed inside the loop instead of being hoisted and held in VGPRs
+    // across the whole launch (the compiler's LICM otherwise pins ~50 VGPRs of
+    // 64-bit per-head offsets).
+    int Fq = Fp;
+    asm volatile("" : "+s"(Fq));
+    const int KHq = Fq / 8;  // k-steps per head-half (4 * Fq / 32)
+    const int ZSq = 4 * Fq + 8;
     float* rsc = rsc0 + (it & 1) * kTile;
     int* rid = rid0 + (it & 1) * kTile;
-    // ---- phase A: each destination -> its fp16 hi/lo row of the Z tile ----
-#pragma unroll
-    for (int d = 0; d < DPW; ++d) {
-      const int r = wave * DPW + d;
-      float z[H][KF];
-      pipe_compute<KF>(pc[d], dd[d], x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, z);
-      const int ri = pc[d].d.x;
-      const float sr = scale_row<KF>(z);
-      write_row<KF>(z, Fp, Zh + r * ZS, Zl + r * ZS);
-      if (lane == 0) {
-        rsc[r] = sr;
-        rid[r] = ri;
-      }
-      // next tile's first batch of this destination slot goes in flight now
-      pc[d] = pn[d];
-      pipe_issue<KF>(pc[d], dd[d], x, ldx, F, col, st, dst_offset);
-      pipe_rec<KF>(pn[d], (t + 2 * G) * kTile + r, num_dst, desc, cols8);
+    // ---- phase A: this wave's destination; next tile's first batch then in flight ----
+    float z[H][KF];
+    pipe_compute<KF>(pc, dd, x, ldx, F, Fq, col, st, slope, dp, seed, zhub, stats, z);
+    const int ri = pc.d.x;
+    pc = pn;
+    pipe_issue<KF>(pc, dd, x, ldx, F, col, st, dst_offset);
+    pipe_rec<KF>(pn, (t + 2 * G) * kTile + wave, num_dst, desc, cols8);
+    const float sr = scale_row<KF>(z);
+    if (lane == 0) {
+      rsc[wave] = sr;
+      rid[wave] = ri;
     }
-    __syncthreads();
-    // ---- phase B: out[16 x 64] = Z[16 x KP] . Wcat on f16 MFMA ----
+    // ---- phase B: out[16 x 64] = Z . Wcat, one head-half at a time ----
     f32x4 acc_m = {0.f, 0.f, 0.f, 0.f}, acc_x = {0.f, 0.f, 0.f, 0.f};
-    const _Float16* ah = Zh + arow * ZS + 8 * akg;
-    const _Float16* al = Zl + arow * ZS + 8 * akg;
-    static_for<0, NKW>([&](auto ui) {
-      constexpr int u = decltype(ui)::value;
-      const int s = kq + KQ * u;
-      if (s < KS) {
-        uint4 blo;
-        if constexpr (u < U0) blo = WL[(s * 4 + ct) * 64 + lane];
-        else blo = wlo[(s * 4 + ct) * 64 + lane];
-        const f16x8 a_hi = *reinterpret_cast<const f16x8*>(ah + 32 * s);
-        const f16x8 a_lo = *reinterpret_cast<const f16x8*>(al + 32 * s);
-        const f16x8 b_hi = *reinterpret_cast<const f16x8*>(&wh[u]);
-        const f16x8 b_lo = *reinterpret_cast<const f16x8*>(&blo);
-        acc_m = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_hi, acc_m, 0, 0, 0);
-        acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_lo, acc_x, 0, 0, 0);
-        acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_lo, b_hi, acc_x, 0, 0, 0);
-      }
-    });
+    const _Float16* ah = Zh + arow * ZSq + 8 * akg;
+    const _Float16* al = Zl + arow * ZSq + 8 * akg;
+    int wofs = (kq * 4 + ct) * 64 + lane;  // fragment index of k-step kq; +1024 per u
+    asm volatile("" : "+v"(wofs));
+#pragma unroll
+    for (int hg = 0; hg < 2; ++hg) {
+      if (hg) __syncthreads();  // half 0 consumed
+      write_half<KF>(z, hg, Fq, Zh + wave * ZSq, Zl + wave * ZSq);
+      __syncthreads();
+      static_for<0, NKW>([&](auto ui) {
+        constexpr int u = decltype(ui)::value;
+        const int s = kq + 4 * u;
+        if (s < 2 * KHq && (s >= KHq) == (hg == 1)) {
+          const int ko = 32 * (s - hg * KHq);
+          const uint4 blo = s < nl ? WL[wofs + 1024 * u] : wlo[wofs + 1024 * u];
+          const f16x8 a_hi = *reinterpret_cast<const f16x8*>(ah + ko);
+          const f16x8 a_lo = *reinterpret_cast<const f16x8*>(al + ko);
+          const f16x8 b_hi = *reinterpret_cast<const f16x8*>(&wh[u]);
+          const f16x8 b_lo = *reinterpret_cast<const f16x8*>(&blo);
+          acc_m = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_hi, acc_m, 0, 0, 0);
+          acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_lo, acc_x, 0, 0, 0);
+          acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_lo, b_hi, acc_x, 0, 0, 0);
+        }
+      });
+    }
     f32x4 accv = acc_m + acc_x * (1.0f / kLoScale);
     if (kq) *reinterpret_cast<f32x4*>(red + (((kq - 1) * 4 + ct) * 64 + lane) * 4) = accv;
-    __syncthreads();  // also: every MFMA of this tile is done before the next Z write
+    __syncthreads();  // partials visible; every read of this tile's half 1 done
     if (!kq) {
 #pragma unroll
-      for (int pp = 0; pp < KQ - 1; ++pp)
+      for (int pp = 0; pp < 3; ++pp)
         accv += *reinterpret_cast<const f32x4*>(red + ((pp * 4 + ct) * 64 + lane) * 4);
       const int n = ct * 16 + (lane & 15);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = (lane >> 4) * 4 + q;
-        const int ri = rid[r];
-        if (ri >= 0) out[int64_t(ri) * C + n] = accv[q] * (rsc[r] * wu) + bcol;
+        const int rr = rid[r];
+        if (rr >= 0) out[int64_t(rr) * C + n] = accv[q] * (rsc[r] * wu) + bcol;
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase A of one tile slot: the normalised z of the slot's destination (all 8
+// heads, fp32, lane <-> feature) or zeros for an empty slot.  Returns the
+// destination row (or -1).
+template <int KF>
+__device__ __forceinline__ int slot_aggregate(
+    int64_t slot, int64_t num_dst, const int4* __restrict__ desc,
+    const int32_t* __restrict__ cols8, const float* __restrict__ x, int64_t ldx, int F, int Fp,
+    const int32_t* __restrict__ col, int64_t dst_offset, const float* __restrict__ st,
+    float slope, float dp, uint64_t seed, const float* __restrict__ zhub,
+    float* __restrict__ stats, float (&z)[H][KF]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) z[hh][q] = 0.f;
+  if (slot >= num_dst) return -1;
+  const int j_first = cols8 ? cols8[slot * 8 + (lane >> 3)] : -1;
+  const int4 dsc = desc[slot];
+  const int i = dsc.x;
+  if (dsc.w >= 0) {  // hub: merged, normalised row from k_hub_merge
+    const float* src = zhub + int64_t(dsc.w) * (H * Fp);
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+      for (int q = 0; q < KF; ++q) {
+        const int f = lane + 64 * q;
+        z[hh][q] = f < Fp ? src[hh * Fp + f] : 0.f;
+      }
+    return i;
+  }
+  const float t_h = st[(dst_offset + i) * 16 + H + (lane & 7)];
+  SegState S =
+      aggregate_segment<KF>(x, ldx, F, col, dsc.y, dsc.z, st, t_h, slope, dp, seed, z, j_first);
+  const float inv_lane = 1.0f / (S.ssum + kSoftmaxEps);
+  if (stats && lane < 8) {
+    stats[int64_t(i) * 16 + lane] = S.m;
+    stats[int64_t(i) * 16 + 8 + lane] = S.ssum;
+  }
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_lane), hh));
+#pragma unroll
+    for (int q = 0; q < KF; ++q) z[hh][q] *= inv;
+  }
+  return i;
+}
+
+// ---------------------------------------------------------------------------
+// 32-row tile kernel: 16 waves, two destinations per wave (rows w and w + 16),
+// so each W fragment streamed from L2 feeds two MFMA row blocks (344 KB of
+// W per 32 destinations at F = 166 instead of per 16).  The half-tile
+// (32 x 4Fp, fp16 hi/lo) is 87 KB: one block per CU.  Heads 4-7 of both rows
+// wait in registers while half 0 is projected.
+template <int KF>
+__global__ void __launch_bounds__(1024, 4) k_tile32(
+    const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
+    int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
+    const int32_t* __restrict__ cols8, const float* __restrict__ st,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ whi,
+    const uint4* __restrict__ wlo, const float* __restrict__ bias, float slope, float dp,
+    uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
+    float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
+  const int ct = wave & 3, kq = wave >> 2;
+  const int64_t base = int64_t(blockIdx.x) * 32;
+
+  // ---- phase A: rows wave and wave + 16 ----
+  float zk[2][4][KF];  // heads 4..7 of both rows, scaled
+  int rows[2];
+  float rsc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    float z[H][KF];
+    rows[d] = slot_aggregate<KF>(base + wave + 16 * d, num_dst, desc, cols8, x, ldx, F, Fp, col,
+                                 dst_offset, st, slope, dp, seed, zhub, stats, z);
+    rsc[d] = scale_row<KF>(z);
+    int Fq = Fp;
+    asm volatile("" : "+s"(Fq));
+    const int ZSq = 4 * Fq + 8;
+    _Float16* Zh = reinterpret_cast<_Float16*>(smem);
+    write_half<KF>(z, 0, Fq, Zh + (wave + 16 * d) * ZSq, Zh + (32 + wave + 16 * d) * ZSq);
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh)
+#pragma unroll
+      for (int q = 0; q < KF; ++q) zk[d][hh][q] = z[4 + hh][q];
+  }
+  int Fq = Fp;
+  asm volatile("" : "+s"(Fq));
+  const int ZSq = 4 * Fq + 8, KHq = Fq / 8;
+  _Float16* Zh = reinterpret_cast<_Float16*>(smem);    // [32][ZS]
+  _Float16* Zl = Zh + 32 * ZSq;                        // [32][ZS]
+  float* red = reinterpret_cast<float*>(Zl + 32 * ZSq);  // [3][4][64][8]
+  float* rscale = red + 3 * 4 * 64 * 8;                // [32]
+  int* rowid = reinterpret_cast<int*>(rscale + 32);    // [32]
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      rscale[wave + 16 * d] = rsc[d];
+      rowid[wave + 16 * d] = rows[d];
+    }
+  }
+
+  // ---- phase B: out[32 x 64] = Z . Wcat, two head-halves ----
+  const int arow = lane & 15, akg = lane >> 4;
+  f32x4 am0 = {0.f, 0.f, 0.f, 0.f}, ax0 = am0, am1 = am0, ax1 = am0;
+  const _Float16* zb0 = Zh + arow * ZSq + 8 * akg;
+  const _Float16* zl0 = Zl + arow * ZSq + 8 * akg;
+  const _Float16* zb1 = zb0 + 16 * ZSq;
+  const _Float16* zl1 = zl0 + 16 * ZSq;
+#pragma unroll
+  for (int hg = 0; hg < 2; ++hg) {
+    const int gs0 = hg * KHq;
+    uint4 bh = {0, 0, 0, 0}, bl = {0, 0, 0, 0};
+    if (kq < KHq) {
+      bh = whi[((gs0 + kq) * 4 + ct) * 64 + lane];
+      bl = wlo[((gs0 + kq) * 4 + ct) * 64 + lane];
+    }
+    if (hg) {
+      __syncthreads();  // half 0 fully consumed
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int r = wave + 16 * d;
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh)
+#pragma unroll
+          for (int q = 0; q < KF; ++q) {
+            const int f = lane + 64 * q;
+            if (f < Fq) {
+              const float v = zk[d][hh][q];
+              const _Float16 hv = (_Float16)v;
+              Zh[r * ZSq + hh * Fq + f] = hv;
+              Zl[r * ZSq + hh * Fq + f] = (_Float16)((v - (float)hv) * kLoScale);
+            }
+          }
+      }
+    }
+    __syncthreads();
+    for (int s = kq; s < KHq; s += 4) {
+      uint4 nh = {0, 0, 0, 0}, nlo = {0, 0, 0, 0};
+      if (s + 4 < KHq) {
+        nh = whi[((gs0 + s + 4) * 4 + ct) * 64 + lane];
+        nlo = wlo[((gs0 + s + 4) * 4 + ct) * 64 + lane];
+      }
+      const f16x8 bhi = *reinterpret_cast<const f16x8*>(&bh);
+      const f16x8 blo = *reinterpret_cast<const f16x8*>(&bl);
+      const f16x8 a0h = *reinterpret_cast<const f16x8*>(zb0 + 32 * s);
+      const f16x8 a0l = *reinterpret_cast<const f16x8*>(zl0 + 32 * s);
+      const f16x8 a1h = *reinterpret_cast<const f16x8*>(zb1 + 32 * s);
+      const f16x8 a1l = *reinterpret_cast<const f16x8*>(zl1 + 32 * s);
+      am0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, bhi, am0, 0, 0, 0);
+      am1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1h, bhi, am1, 0, 0, 0);
+      ax0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, blo, ax0, 0, 0, 0);
+      ax1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1h, blo, ax1, 0, 0, 0);
+      ax0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0l, bhi, ax0, 0, 0, 0);
+      ax1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1l, bhi, ax1, 0, 0, 0);
+      bh = nh;
+      bl = nlo;
+    }
+  }
+  f32x4 acc0 = am0 + ax0 * (1.0f / kLoScale);
+  f32x4 acc1 = am1 + ax1 * (1.0f / kLoScale);
+  if (kq) {
+    float* rp = red + (((kq - 1) * 4 + ct) * 64 + lane) * 8;
+    *reinterpret_cast<f32x4*>(rp) = acc0;
+    *reinterpret_cast<f32x4*>(rp + 4) = acc1;
+  }
+  __syncthreads();
+  if (!kq) {
+#pragma unroll
+    for (int pp = 0; pp < 3; ++pp) {
+      const float* rp = red + ((pp * 4 + ct) * 64 + lane) * 8;
+      acc0 += *reinterpret_cast<const f32x4*>(rp);
+      acc1 += *reinterpret_cast<const f32x4*>(rp + 4);
+    }
+    const int n = ct * 16 + (lane & 15);
+    const float b = bias ? bias[n] : 0.f;
+    const float wu = hdr->w_unscale;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (lane >> 4) * 4 + q;
+      const int r0 = rowid[r], r1 = rowid[16 + r];
+      if (r0 >= 0) out[int64_t(r0) * C + n] = acc0[q] * (rscale[r] * wu) + b;
+      if (r1 >= 0) out[int64_t(r1) * C + n] = acc1[q] * (rscale[16 + r] * wu) + b;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Two destinations aggregated concurrently by one wave: both slot records and
+// first-batch columns load in one round trip, both first batches of x rows in
+// the next, so twice the rows are in flight per wave compared with
+// aggregate_segment.  Same arithmetic per destination as aggregate_segment
+// (online softmax over batches of 8 messages, rows in sub-batches of 4).
+template <int KF>
+struct PairSeg {
+  int e0, n;    // CSR start and message count (n = 0: nothing to aggregate)
+  int jf;       // prefetched column of message (lane >> 3) of the first batch, or -1
+  float t;      // t_i for head lane & 7
+  float m, l;   // running max (head lane & 7), running denominator (per lane)
+};
+
+template <int KF>
+__device__ __forceinline__ void pair_logits(PairSeg<KF>& S, int b, bool first,
+                                            const int32_t* __restrict__ col,
+                                            const float* __restrict__ st, float slope, float dp,
+                                            uint64_t seed, float (&z)[H][KF], int& j, float& p) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  const bool valid = b + kk < S.n;
+  const int e = S.e0 + min(b + kk, S.n - 1);
+  j = (first && S.jf >= 0) ? S.jf : col[e];
+  const float v = leaky(st[int64_t(j) * 16 + h] + S.t, slope);
+  float bm = valid ? v : -INFINITY;
+  bm = fmaxf(bm, __shfl_xor(bm, 8));
+  bm = fmaxf(bm, __shfl_xor(bm, 16));
+  bm = fmaxf(bm, __shfl_xor(bm, 32));
+  const float mn = fmaxf(S.m, bm);
+  const float sc = __expf(S.m - mn);
+  p = valid ? __expf(v - mn) : 0.f;
+  S.l = fmaf(S.l, sc, p);
+  if (!first && __any(sc != 1.0f)) {
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) {
+      const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
+#pragma unroll
+      for (int q = 0; q < KF; ++q) z[hh][q] *= s;
+    }
+  }
+  S.m = mn;
+  if (dp > 0.f)
+    p = dropout_keep(seed, uint32_t(S.e0 + b + kk), uint32_t(h), dp) ? p * (1.0f / (1.0f - dp)) : 0.f;
+}
+
+template <int KF>
+__device__ __forceinline__ void pair_rows(const float* __restrict__ x, int64_t ldx, int F, int j,
+                                          int k0, float (&xv)[4][KF]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int jk = __builtin_amdgcn_readlane(j, 8 * (k0 + k));
+    const float* xr = x + int64_t(jk) * ldx;
+#pragma unroll
+    for (int q = 0; q < KF; ++q) {
+      const int f = lane + 64 * q;
+      const float t = xr[f < F ? f : F - 1];
+      xv[k][q] = f < F ? t : 0.f;
+    }
+  }
+}
+
+template <int KF>
+__device__ __forceinline__ void pair_fma(float p, int k0, const float (&xv)[4][KF],
+                                         float (&z)[H][KF]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) {
+      const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 8 * (k0 + k) + hh));
+#pragma unroll
+      for (int q = 0; q < KF; ++q) z[hh][q] = fmaf(pk, xv[k][q], z[hh][q]);
+    }
+}
+
+// 32-row tiles (rows w and w + 16 of a tile go to wave w) with both rows'
+// aggregation interleaved; phase B as k_tile32.
+template <int KF>
+__global__ void __launch_bounds__(1024, 4) k_pair(
+    const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
+    int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
+    const int32_t* __restrict__ cols8, const float* __restrict__ st,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ whi,
+    const uint4* __restrict__ wlo, const float* __restrict__ bias, float slope, float dp,
+    uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
+    float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
+  const int ct = wave & 3, kq = wave >> 2;
+  const int64_t base = int64_t(blockIdx.x) * 32;
+
+  // ---- phase A: rows wave (a) and wave + 16 (b), interleaved ----
+  float za[H][KF], zb[H][KF];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) za[hh][q] = zb[hh][q] = 0.f;
+  const int64_t sa = base + wave, sb = base + wave + 16;
+  int4 da = make_int4(-1, 0, 0, -1), db = make_int4(-1, 0, 0, -1);
+  PairSeg<KF> A, B;
+  A.jf = B.jf = -1;
+  if (sa < num_dst) {
+    if (cols8) A.jf = cols8[sa * 8 + (lane >> 3)];
+    da = desc[sa];
+  }
+  if (sb < num_dst) {
+    if (cols8) B.jf = cols8[sb * 8 + (lane >> 3)];
+    db = desc[sb];
+  }
+  const bool agg_a = da.x >= 0 && da.w < 0, agg_b = db.x >= 0 && db.w < 0;
+  A.e0 = da.y; A.n = agg_a ? da.z - da.y : 0;
+  B.e0 = db.y; B.n = agg_b ? db.z - db.y : 0;
+  A.t = agg_a ? st[(dst_offset + da.x) * 16 + H + (lane & 7)] : 0.f;
+  B.t = agg_b ? st[(dst_offset + db.x) * 16 + H + (lane & 7)] : 0.f;
+  A.m = B.m = -INFINITY;
+  A.l = B.l = 0.f;
+  const int len = max(A.n, B.n);
+  for (int b = 0; b < len; b += 8) {
+    const bool first = b == 0;
+    const bool act_a = b < A.n, act_b = b < B.n;
+    int ja = 0, jb = 0;
+    float pa = 0.f, pb = 0.f;
+    if (act_a) pair_logits<KF>(A, b, first, col, st, slope, dp, seed, za, ja, pa);
+    if (act_b) pair_logits<KF>(B, b, first, col, st, slope, dp, seed, zb, jb, pb);
+    const int nka = act_a ? min(8, A.n - b) : 0, nkb = act_b ? min(8, B.n - b) : 0;
+    for (int k0 = 0; k0 < max(nka, nkb); k0 += 4) {
+      float xa[4][KF], xb[4][KF];
+      if (k0 < nka) pair_rows<KF>(x, ldx, F, ja, k0, xa);
+      if (k0 < nkb) pair_rows<KF>(x, ldx, F, jb, k0, xb);
+      if (k0 < nka) pair_fma<KF>(pa, k0, xa, za);
+      if (k0 < nkb) pair_fma<KF>(pb, k0, xb, zb);
+    }
+  }
+  int rows[2] = {da.x, db.x};
+  float rsc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    float (&z)[H][KF] = d ? zb : za;
+    const int4 dd = d ? db : da;
+    PairSeg<KF>& S = d ? B : A;
+    if (dd.x >= 0 && dd.w >= 0) {  // hub: merged, normalised row
+      int Fq = Fp;
+      asm volatile("" : "+s"(Fq));
+      const float* src = zhub + int64_t(dd.w) * (H * Fq);
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+        for (int q = 0; q < KF; ++q) {
+          const int f = lane + 64 * q;
+          z[hh][q] = f < Fq ? src[hh * Fq + f] : 0.f;
+        }
+    } else if (dd.x >= 0) {
+      float l = S.l;
+      l += __shfl_xor(l, 8);
+      l += __shfl_xor(l, 16);
+      l += __shfl_xor(l, 32);
+      if (stats && lane < 8) {
+        stats[int64_t(dd.x) * 16 + lane] = S.m;
+        stats[int64_t(dd.x) * 16 + 8 + lane] = l;
+      }
+      const float inv_lane = 1.0f / (l + kSoftmaxEps);
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_lane), hh));
+#pragma unroll
+        for (int q = 0; q < KF; ++q) z[hh][q] *= inv;
+      }
+    }
+    rsc[d] = scale_row<KF>(z);
+  }
+  int Fq = Fp;
+  asm volatile("" : "+s"(Fq));
+  const int ZSq = 4 * Fq + 8, KHq = Fq / 8;
+  _Float16* Zh = reinterpret_cast<_Float16*>(smem);    // [32][ZS]
+  _Float16* Zl = Zh + 32 * ZSq;                        // [32][ZS]
+  float* red = reinterpret_cast<float*>(Zl + 32 * ZSq);  // [3][4][64][8]
+  float* rscale = red + 3 * 4 * 64 * 8;                // [32]
+  int* rowid = reinterpret_cast<int*>(rscale + 32);    // [32]
+  write_half<KF>(za, 0, Fq, Zh + wave * ZSq, Zl + wave * ZSq);
+  write_half<KF>(zb, 0, Fq, Zh + (wave + 16) * ZSq, Zl + (wave + 16) * ZSq);
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      rscale[wave + 16 * d] = rsc[d];
+      rowid[wave + 16 * d] = rows[d];
+    }
+  }
+
+  // ---- phase B: out[32 x 64] = Z . Wcat, two head-halves ----
+  const int arow = lane & 15, akg = lane >> 4;
+  f32x4 am0 = {0.f, 0.f, 0.f, 0.f}, ax0 = am0, am1 = am0, ax1 = am0;
+  const _Float16* zb0 = Zh + arow * ZSq + 8 * akg;
+  const _Float16* zl0 = Zl + arow * ZSq + 8 * akg;
+  const _Float16* zb1 = zb0 + 16 * ZSq;
+  const _Float16* zl1 = zl0 + 16 * ZSq;
+#pragma unroll
+  for (int hg = 0; hg < 2; ++hg) {
+    const int gs0 = hg * KHq;
+    uint4 bh = {0, 0, 0, 0}, bl = {0, 0, 0, 0};
+    if (kq < KHq) {
+      bh = whi[((gs0 + kq) * 4 + ct) * 64 + lane];
+      bl = wlo[((gs0 + kq) * 4 + ct) * 64 + lane];
+    }
+    if (hg) {
+      __syncthreads();  // half 0 fully consumed
+      write_half<KF>(za, 1, Fq, Zh + wave * ZSq, Zl + wave * ZSq);
+      write_half<KF>(zb, 1, Fq, Zh + (wave + 16) * ZSq, Zl + (wave + 16) * ZSq);
+    }
+    __syncthreads();
+    for (int s = kq; s < KHq; s += 4) {
+      uint4 nh = {0, 0, 0, 0}, nlo = {0, 0, 0, 0};
+      if (s + 4 < KHq) {
+        nh = whi[((gs0 + s + 4) * 4 + ct) * 64 + lane];
+        nlo = wlo[((gs0 + s + 4) * 4 + ct) * 64 + lane];
+      }
+      const f16x8 bhi = *reinterpret_cast<const f16x8*>(&bh);
+      const f16x8 blo = *reinterpret_cast<const f16x8*>(&bl);
+      const f16x8 a0h = *reinterpret_cast<const f16x8*>(zb0 + 32 * s);
+      const f16x8 a0l = *reinterpret_cast<const f16x8*>(zl0 + 32 * s);
+      const f16x8 a1h = *reinterpret_cast<const f16x8*>(zb1 + 32 * s);
+      const f16x8 a1l = *reinterpret_cast<const f16x8*>(zl1 + 32 * s);
+      am0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, bhi, am0, 0, 0, 0);
+      am1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1h, bhi, am1, 0, 0, 0);
+      ax0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0h, blo, ax0, 0, 0, 0);
+      ax1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1h, blo, ax1, 0, 0, 0);
+      ax0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0l, bhi, ax0, 0, 0, 0);
+      ax1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1l, bhi, ax1, 0, 0, 0);
+      bh = nh;
+      bl = nlo;
+    }
+  }
+  f32x4 acc0 = am0 + ax0 * (1.0f / kLoScale);
+  f32x4 acc1 = am1 + ax1 * (1.0f / kLoScale);
+  if (kq) {
+    float* rp = red + (((kq - 1) * 4 + ct) * 64 + lane) * 8;
+    *reinterpret_cast<f32x4*>(rp) = acc0;
+    *reinterpret_cast<f32x4*>(rp + 4) = acc1;
+  }
+  __syncthreads();
+  if (!kq) {
+#pragma unroll
+    for (int pp = 0; pp < 3; ++pp) {
+      const float* rp = red + ((pp * 4 + ct) * 64 + lane) * 8;
+      acc0 += *reinterpret_cast<const f32x4*>(rp);
+      acc1 += *reinterpret_cast<const f32x4*>(rp + 4);
+    }
+    const int n = ct * 16 + (lane & 15);
+    const float bb = bias ? bias[n] : 0.f;
+    const float wu = hdr->w_unscale;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (lane >> 4) * 4 + q;
+      const int r0 = rowid[r], r1 = rowid[16 + r];
+      if (r0 >= 0) out[int64_t(r0) * C + n] = acc0[q] * (rscale[r] * wu) + bb;
+      if (r1 >= 0) out[int64_t(r1) * C + n] = acc1[q] * (rscale[16 + r] * wu) + bb;
     }
   }
 }
@@ -958,7 +1421,8 @@ int fused_mode() {
   return m;
 }
 
-// GFD_TILE_KERNEL (A/B switch): 0 default (k_fused), 2 persistent weight-stationary.
+// GFD_TILE_KERNEL (A/B switch): 0 default (k_fused), 2 persistent weight-stationary,
+// 3 32-row tiles, 4 32-row tiles with paired aggregation.
 int tile_kernel() {
   static int m = [] {
     const char* e = getenv("GFD_TILE_KERNEL");
@@ -988,24 +1452,27 @@ struct AggArgs {
 
 constexpr size_t kLdsBytes = 160 * 1024;
 
-size_t persist_fixed_lds(int Fp, int kphases) {
-  return align_up(sizeof(_Float16) * 2 * kTile * (H * Fp + 8), 16) +
-         sizeof(float) * (kphases - 1) * 4 * 64 * 4 + sizeof(float) * 4 * kTile;
+size_t persist_fixed_lds(int Fp) {  // fp16 hi/lo half-tile + partials + row scale/ids
+  return sizeof(_Float16) * 2 * kTile * (4 * Fp + 8) + sizeof(float) * 3 * 4 * 64 * 4 +
+         sizeof(float) * 4 * kTile;
 }
 
 template <int KF>
 gfd_status launch_persist(const AggArgs& a, const PackLayout& L, int64_t tiles,
                           hipStream_t stream) {
-  // per feature-chunk class: waves per block, k-steps per wave, LDS-resident W_lo groups
-  constexpr int WAVES = KF == 3 ? 8 : 16;
-  constexpr int KQ = WAVES / 4;
-  constexpr int NKW = (KF * 64 * H / 32 + KQ - 1) / KQ;
-  constexpr int U0 = KF == 1 ? 4 : (KF == 2 ? 5 : 8);
-  const size_t lds = persist_fixed_lds(L.Fp, KQ) + size_t(KQ * U0) * sizeof(uint4) * 256;
-  if (lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;
+#ifdef EXP_NKW
+  constexpr int NKW = EXP_NKW;
+#else
+  constexpr int NKW = (KF * 64 * H / 32 + 3) / 4;   // W_hi k-steps per wave (all of them)
+#endif
+  const size_t fixed = persist_fixed_lds(L.Fp);
+  if (fixed > kLdsBytes) return GFD_ERR_UNSUPPORTED;
+  int nl = int((kLdsBytes - fixed) / (sizeof(uint4) * 256));  // W_lo k-steps held in LDS
+  if (nl > L.KS) nl = L.KS;
+  const size_t lds = fixed + size_t(nl) * sizeof(uint4) * 256;
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_persist<KF, WAVES, NKW, U0>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_persist<KF, NKW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsBytes)) !=
         hipSuccess)
       return GFD_ERR_HIP;
@@ -1017,9 +1484,9 @@ gfd_status launch_persist(const AggArgs& a, const PackLayout& L, int64_t tiles,
   const PackHeader* hdr = reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off);
   const uint4* whi = reinterpret_cast<const uint4*>(a.packed + L.whi_off);
   const uint4* wlo = reinterpret_cast<const uint4*>(a.packed + L.wlo_off);
-  k_persist<KF, WAVES, NKW, U0><<<int(grid), WAVES * 64, lds, stream>>>(
+  k_persist<KF, NKW><<<int(grid), kPWaves * 64, lds, stream>>>(
       a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
-      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st, hdr, whi, wlo, a.bias,
+      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st, hdr, whi, wlo, nl, a.bias,
       a.slope, a.dp, a.seed, a.zhub, a.out, a.stats, tiles);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
@@ -1046,6 +1513,30 @@ gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t s
   const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
   if constexpr (KF <= 3) {
     if (p.slot_desc && tile_kernel() == 2) return launch_persist<KF>(a, L, tiles, stream);
+    if (p.slot_desc && (tile_kernel() == 3 || tile_kernel() == 4)) {
+      auto kern = tile_kernel() == 4 ? &k_pair<KF> : &k_tile32<KF>;
+      const size_t lds = sizeof(_Float16) * 2 * 32 * (4 * Fp + 8) + sizeof(float) * (3 * 4 * 64 * 8 + 64);
+      static bool attr_set = false;
+      if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tile32<KF>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsBytes)) !=
+                hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pair<KF>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsBytes)) !=
+                hipSuccess)
+          return GFD_ERR_HIP;
+        attr_set = true;
+      }
+      const PackHeader* hdr = reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off);
+      kern<<<int((a.num_dst + 31) / 32), 1024, lds, stream>>>(
+          a.x, a.F, Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
+          reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st, hdr,
+          reinterpret_cast<const uint4*>(a.packed + L.whi_off),
+          reinterpret_cast<const uint4*>(a.packed + L.wlo_off), a.bias, a.slope, a.dp, a.seed,
+          a.zhub, a.out, a.stats);
+      GFD_LAUNCH_CHECK();
+      return GFD_OK;
+    }
   }
   const PackHeader* hdr = reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off);
   const uint4* whi = reinterpret_cast<const uint4*>(a.packed + L.whi_off);
@@ -1053,7 +1544,7 @@ gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t s
   auto kern = fused_occ(KF) == 4 ? &k_fused<KF, 4> : &k_fused<KF, 8>;
   kern<<<int(tiles), kFusedWaves * 64, fused_smem(Fp), stream>>>(
       a.x, a.F, Fp, a.ldx, a.rowptr, a.col, a.num_dst, a.dst_offset, p.row_order,
-      reinterpret_cast<const int4*>(p.slot_desc), a.st, hdr,
+      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st, hdr,
       whi, wlo, a.bias, a.slope, a.dp, a.seed, p.num_hubs > 0 ? p.hub_rank : nullptr, a.zhub,
       a.out, a.stats, fused_mode());
   GFD_LAUNCH_CHECK();
