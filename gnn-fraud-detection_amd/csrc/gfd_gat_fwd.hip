@@ -36,7 +36,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 struct PackLayout {
   int F, Fp, Fu, KP, KS, KH;
-  size_t hdr_off, uv_off, whi_off, wlo_off, bytes;
+  size_t hdr_off, uv_off, whi_off, wlo_off, wsh_off, wsl_off, bytes;
 };
 
 inline PackLayout pack_layout(int F) {
@@ -52,6 +52,9 @@ inline PackLayout pack_layout(int F) {
   L.uv_off = o; o = align_up(o + sizeof(float) * 2 * H * L.Fu, 256);
   L.whi_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
   L.wlo_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
+  // feature-major fragments for k_stream: K position p = 8 f + h, unscaled lo
+  L.wsh_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
+  L.wsl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
   L.bytes = o;
   return L;
 }
@@ -118,6 +121,30 @@ __global__ void k_pack_frag(const float* __restrict__ W, int F, int Fp, int KS,
   }
   whi[idx] = hi.v;
   wlo[idx] = lo.v;
+}
+
+// Feature-major fragments for k_stream: K position p = 8 f + h (one 16-B Z store
+// per feature holds all 8 heads), lo = v - hi unscaled (|lo| <= 2^3 for the
+// 2^14-scaled W; fp16 subnormals there cost < 2^-38 of the largest weight).
+__global__ void k_pack_frag_s(const float* __restrict__ W, int F, int KS,
+                              const PackHeader* __restrict__ hdr, uint4* __restrict__ wsh,
+                              uint4* __restrict__ wsl) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (s, ct, lane)
+  if (idx >= KS * 4 * 64) return;
+  int lane = idx & 63, ct = (idx >> 6) & 3, s = idx >> 8;
+  int n = ct * 16 + (lane & 15);
+  int f = 4 * s + (lane >> 4);
+  const float sc = hdr->w_scale * (1.0f / H);
+  union { uint4 v; _Float16 h[8]; } hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = (f < F) ? W[size_t(j * C + n) * F + f] * sc : 0.f;
+    _Float16 hv = (_Float16)v;
+    hi.h[j] = hv;
+    lo.h[j] = (_Float16)(v - (float)hv);
+  }
+  wsh[idx] = hi.v;
+  wsl[idx] = lo.v;
 }
 
 // ---------------------------------------------------------------------------
@@ -570,9 +597,10 @@ __device__ __forceinline__ void pipe_compute(const DstPipe& p, const DstData<KF>
   for (int hh = 0; hh < H; ++hh)
 #pragma unroll
     for (int qq = 0; qq < KF; ++qq) z[hh][qq] = 0.f;
-  if (p.d.x < 0) return;
-  if (p.d.w >= 0) {  // hub: merged row (already normalised)
-    const float* src = zhub + int64_t(p.d.w) * (H * Fp);
+  const int4 d = p.d;
+  if (d.x < 0) return;
+  if (d.w >= 0) {  // hub: merged row (already normalised)
+    const float* src = zhub + int64_t(d.w) * (H * Fp);
 #pragma unroll
     for (int hh = 0; hh < H; ++hh)
 #pragma unroll
@@ -651,8 +679,8 @@ __device__ __forceinline__ void pipe_compute(const DstPipe& p, const DstData<KF>
   l += __shfl_xor(l, 16);
   l += __shfl_xor(l, 32);
   if (stats && lane < 8) {
-    stats[int64_t(p.d.x) * 16 + lane] = m;
-    stats[int64_t(p.d.x) * 16 + 8 + lane] = l;
+    stats[int64_t(d.x) * 16 + lane] = m;
+    stats[int64_t(d.x) * 16 + 8 + lane] = l;
   }
   const float inv_lane = 1.0f / (l + kSoftmaxEps);
 #pragma unroll
@@ -1272,6 +1300,434 @@ __global__ void __launch_bounds__(1024, 4) k_pair(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Weight-stationary streaming tile kernel (persistent, one 8-wave block per CU,
+// two waves per SIMD at up to 256 VGPRs).
+//
+//  * The whole projection (fp16 W_hi and W_lo B-fragments, 344 KB at F = 166)
+//    lives in registers for the launch: wave w owns the k-steps
+//    [NM*w, NM*w + NM) for all four column tiles plus NE "extra" units
+//    (k-step 8*NM + (w >> 2) + 2v, column tile w & 3).  Nothing but x rows,
+//    logits and slot records streams from memory per tile.
+//  * Z goes through LDS once per 16-row tile in the feature-major K order
+//    p = 8 f + h, so a lane stores all 8 heads of its feature with one 16-B
+//    write per (hi, lo).  Single accumulator per column tile:
+//    acc += Zhi.Whi + Zhi.Wlo + Zlo.Whi (lo parts unscaled).
+//  * Two destinations per wave (rows 2w, 2w+1); their first batches of x rows
+//    are issued one tile ahead, so they are in flight during the MFMA phase and
+//    the cross-wave reduction of the previous tile.
+//  * Per tile: MFMA -> partials to LDS -> barrier -> reduce + store out (waves
+//    0-3, one column tile each) and aggregate the next tile's rows into Z ->
+//    barrier.
+constexpr int kSWaves = 8;
+
+// The stream kernel's helpers take the lane index as an argument: the kernel
+// launders it (asm) once per tile, so no per-lane address derived from it can
+// be hoisted out of the persistent loop and pinned in VGPRs for the whole
+// launch (the registers belong to the stationary weights).
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm queue)
+  int4 d;         // {row, e_begin, e_end, hub_rank}
+  int j;          // source of message (lane >> 3) of the first batch
+  bool live;      // slot < num_dst (otherwise d / j are a clamped copy, row taken as -1)
+};
+
+__device__ __forceinline__ int4 uni4(int4 v) {
+  return make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                   __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+}
+
+struct SlotRing {  // the same record parked in LDS between issue and aggregation
+  int4 d;
+  int j[8];
+};
+
+template <int KF>
+struct SlotRows {  // first batch in flight
+  static constexpr int PF = KF >= 3 ? 2 : 4;  // rows issued ahead (register budget)
+  float th;        // t_i of head lane & 7
+  float sj;        // s_j of the lane's message
+  float xv[PF][KF];  // x rows of messages 0..PF-1 (lane <-> feature)
+};
+
+__device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst,
+                                       const int4* __restrict__ desc,
+                                       const int32_t* __restrict__ cols8, int lane) {
+  const int64_t sl = slot < num_dst ? slot : num_dst - 1;
+  const int z0 = opaque(0);  // divergent zero: a vector load, not s_load
+  p.d = desc[sl + z0];
+  p.j = cols8[sl * 8 + (lane >> 3)];
+  p.live = slot < num_dst;
+}
+
+// Row loads land straight in the destination registers with nothing consuming
+// them here: any use (even a select) in the issuing block would make the
+// compiler wait for the load on the spot.  Lanes f >= F read x[F - 1]; those
+// Z entries meet zero weight rows, so they need no masking.
+template <int KF>
+__device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int lane,
+                                        float (&v)[KF]) {
+#pragma unroll
+  for (int q = 0; q < KF; ++q) {
+    const int f = lane + 64 * q;
+    v[q] = xr[f < F ? f : F - 1];
+  }
+}
+
+// Issue the first batch of a slot (4 rows, t_i, s_j) unconditionally (empty and
+// hub slots read valid rows that are ignored, so no branch joins in-flight
+// loads) and park the record in the LDS ring for the aggregation.
+template <int KF>
+__device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF>& q,
+                                         const float* __restrict__ x, int64_t ldx, int F,
+                                         const float* __restrict__ st, int64_t dst_offset,
+                                         SlotRing* __restrict__ ring, int lane) {
+  const int h = lane & 7;
+  const int row = __builtin_amdgcn_readfirstlane(p.d.x);  // >= 0: clamped slots are real rows
+  q.th = st[(dst_offset + row) * 16 + H + h];
+  q.sj = st[int64_t(p.j) * 16 + h];
+#pragma unroll
+  for (int k = 0; k < SlotRows<KF>::PF; ++k) {
+    const int jk = __builtin_amdgcn_readlane(p.j, 8 * k);
+    sl_rows<KF>(x + int64_t(jk) * ldx, F, lane, q.xv[k]);
+  }
+  if (lane == 0) ring->d = make_int4(p.live ? p.d.x : -1, p.d.y, p.d.z, p.d.w);
+  if (h == 0) ring->j[lane >> 3] = p.j;
+}
+
+// Normalised z of one slot (all 8 heads, lane <-> feature); online softmax over
+// batches of 8 messages, rows in sub-batches of 4; the first sub-batch is in q.
+template <int KF>
+__device__ __forceinline__ void sl_compute(const int4 d, const int j0, const SlotRows<KF>& q,
+                                           const float* __restrict__ x, int64_t ldx, int F,
+                                           int Fp, const int32_t* __restrict__ col,
+                                           const float* __restrict__ st, float slope, float dp,
+                                           uint64_t seed, const float* __restrict__ zhub,
+                                           float* __restrict__ stats, int lane,
+                                           float (&z)[H][KF]) {
+  const int h = lane & 7, kk = lane >> 3;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[hh][qq] = 0.f;
+  if (d.x < 0) return;
+  if (d.w >= 0) {  // hub: merged row (already normalised)
+    const float* src = zhub + int64_t(d.w) * (H * Fp);
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq) {
+        const int f = lane + 64 * qq;
+        z[hh][qq] = f < Fp ? src[hh * Fp + f] : 0.f;
+      }
+    return;
+  }
+  const int e0 = d.y, e1 = d.z;
+  float m = -INFINITY, l = 0.f;
+  for (int b = e0; b < e1; b += 8) {
+    const int e = b + kk;
+    const bool valid = e < e1;
+    int j;
+    float v;
+    if (b == e0) {
+      j = j0;
+      v = leaky(q.sj + q.th, slope);
+    } else {
+      j = col[valid ? e : e1 - 1];
+      v = leaky(st[int64_t(j) * 16 + h] + q.th, slope);
+    }
+    float bm = valid ? v : -INFINITY;
+    bm = fmaxf(bm, __shfl_xor(bm, 8));
+    bm = fmaxf(bm, __shfl_xor(bm, 16));
+    bm = fmaxf(bm, __shfl_xor(bm, 32));
+    const float mn = fmaxf(m, bm);
+    const float sc = __expf(m - mn);
+    float pv = valid ? __expf(v - mn) : 0.f;
+    l = fmaf(l, sc, pv);
+    if (b != e0 && __any(sc != 1.0f)) {
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
+#pragma unroll
+        for (int qq = 0; qq < KF; ++qq) z[hh][qq] *= s;
+      }
+    }
+    m = mn;
+    if (dp > 0.f)
+      pv = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? pv * (1.0f / (1.0f - dp)) : 0.f;
+    const int nk = min(8, e1 - b);
+    for (int k0 = 0; k0 < nk; k0 += 4) {
+      float xl[4][KF];
+      constexpr int PF = SlotRows<KF>::PF;
+      if (b == e0 && k0 == 0) {
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+#pragma unroll
+          for (int qq = 0; qq < KF; ++qq) xl[k][qq] = q.xv[k][qq];
+        if (PF < 4 && nk > PF) {
+#pragma unroll
+          for (int k = PF; k < 4; ++k) {
+            const int jk = __builtin_amdgcn_readlane(j, 8 * k);
+            sl_rows<KF>(x + int64_t(jk) * ldx, F, lane, xl[k]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int jk = __builtin_amdgcn_readlane(j, 8 * (k0 + k));
+          sl_rows<KF>(x + int64_t(jk) * ldx, F, lane, xl[k]);
+        }
+      }
+      const int kn = min(4, nk - k0);  // padding rows carry p = 0 anyway
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k == 0 || k < kn) {
+#pragma unroll
+          for (int hh = 0; hh < H; ++hh) {
+            const float pk =
+                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), 8 * (k0 + k) + hh));
+#pragma unroll
+            for (int qq = 0; qq < KF; ++qq) z[hh][qq] = fmaf(pk, xl[k][qq], z[hh][qq]);
+          }
+        }
+      }
+    }
+  }
+  l += __shfl_xor(l, 8);
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  if (stats && lane < 8) {
+    stats[int64_t(d.x) * 16 + lane] = m;
+    stats[int64_t(d.x) * 16 + 8 + lane] = l;
+  }
+  const float inv_lane = 1.0f / (l + kSoftmaxEps);
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_lane), hh));
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[hh][qq] *= inv;
+  }
+}
+
+// Aggregate one slot (record from the LDS ring, first batch in q) and store its
+// Z row: power-of-two scaled, feature-major (K position 8 f + h), fp16 hi and
+// unscaled lo', one 16-B store per feature each.
+template <int KF>
+__device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, const SlotRows<KF>& q,
+                                         const float* __restrict__ x, int64_t ldx, int F, int Fp,
+                                         const int32_t* __restrict__ col,
+                                         const float* __restrict__ st, float slope, float dp,
+                                         uint64_t seed, const float* __restrict__ zhub,
+                                         float* __restrict__ stats, _Float16* __restrict__ zh,
+                                         _Float16* __restrict__ zl, float* __restrict__ rsc,
+                                         int* __restrict__ rid, int r, int lane) {
+  const int4 d = uni4(ring->d);
+  const int j0 = ring->j[lane >> 3];
+  float z[H][KF];
+  sl_compute<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, lane, z);
+  float zm = 0.f;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) zm = fmaxf(zm, fabsf(z[hh][qq]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) zm = fmaxf(zm, __shfl_xor(zm, o));
+  int ex = 0;
+  if (zm > 0.f) frexpf(zm, &ex);
+  int er = 14 - ex;
+  er = er > 100 ? 100 : (er < -100 ? -100 : er);
+  const float rs = ldexpf(1.0f, er);
+#pragma unroll
+  for (int qq = 0; qq < KF; ++qq) {
+    const int f = lane + 64 * qq;
+    if (f < Fp) {
+      union { f16x8 v; _Float16 h[8]; } a, b;
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        const float v = z[hh][qq] * rs;
+        const _Float16 hv = (_Float16)v;
+        a.h[hh] = hv;
+        b.h[hh] = (_Float16)(v - (float)hv);
+      }
+      *reinterpret_cast<f16x8*>(zh + 8 * f) = a.v;
+      *reinterpret_cast<f16x8*>(zl + 8 * f) = b.v;
+    }
+  }
+  if (lane == 0) {
+    rsc[r] = ldexpf(1.0f, -er);
+    rid[r] = d.x;
+  }
+}
+
+// Weight-stationary streaming tile kernel (persistent, one 8-wave block per CU,
+// two waves per SIMD at up to 256 VGPRs).
+//
+//  * The projection weights stay on chip for the launch: wave w owns column
+//    tile ct = w & 3 over K half kh = w >> 2 (k-steps [kh*KH, kh*KH + KH)):
+//    W_hi of its k-steps in VGPRs, W_lo of the first KH - LO in VGPRs and of
+//    the last LO in LDS.  Only x rows, logits and slot records stream per tile.
+//  * Z goes through LDS once per 16-row tile in the feature-major K order
+//    p = 8 f + h, so a lane stores all 8 heads of its feature with one 16-B
+//    write per (hi, lo).  acc += Zhi.Whi + Zhi.Wlo + Zlo.Whi (lo unscaled).
+//  * Two destinations per wave (rows 2w, 2w+1).  Their first batches of x rows
+//    are issued one tile ahead (in flight during the MFMA phase and the
+//    reduction); their records are loaded two tiles ahead and parked in an LDS
+//    ring between issue and aggregation.  After the rows are issued no load the
+//    kernel waits on precedes their use (vmcnt is in order).
+//  * Per tile: MFMA -> kh = 1 partials to LDS -> barrier -> kh = 0 waves reduce
+//    and store out; every wave aggregates its next rows into Z -> barrier.
+template <int KF, int KHM, int LO>
+__global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
+    const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
+    int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
+    const int32_t* __restrict__ cols8, const float* __restrict__ st,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
+    const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
+    uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
+    float* __restrict__ stats, int64_t num_tiles, int mode) {
+  extern __shared__ __attribute__((aligned(16))) char ssm[];
+  const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
+  const int KH = Fp / 8;                                        // k-steps per K half (<= KHM)
+  _Float16* Zh = reinterpret_cast<_Float16*>(ssm);              // [16][ZS]
+  _Float16* Zl = Zh + kTile * ZS;                               // [16][ZS]
+  f32x4* red = reinterpret_cast<f32x4*>(Zl + kTile * ZS);       // [4 ct][64]
+  SlotRing* ring0 = reinterpret_cast<SlotRing*>(red + 4 * 64);  // [2 parity][16]
+  float* rsc0 = reinterpret_cast<float*>(ring0 + 2 * kTile);    // [2][16] by tile parity
+  int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);         // [2][16]
+  uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);       // [8 waves][LO][64]
+
+  const int wave = wave_uniform(threadIdx.x >> 6);
+  const int ct = wave & 3, kh = wave >> 2;
+  const int r0 = 2 * wave, r1 = r0 + 1;
+  const int64_t G = gridDim.x;
+  const int64_t t0 = blockIdx.x;
+  // tiles t0 + v*G, v < nv
+  const int64_t nv = t0 < num_tiles ? (num_tiles - 1 - t0) / G + 1 : 0;
+  int lane = opaque(threadIdx.x & 63);
+  auto slot = [&](int64_t v, int r) { return (t0 + v * G) * kTile + r; };
+
+  // kernel-lifetime constants first: nothing the loop waits on may be loaded
+  // after the first rows are issued
+  const float bcol = bias ? bias[ct * 16 + (lane & 15)] : 0.f;
+  const float wu = hdr->w_unscale;
+  constexpr int NR = KHM - LO;  // k-steps (of KHM) with W_lo in registers
+  f16x8 bh[KHM], bl[NR > 0 ? NR : 1];
+#pragma unroll
+  for (int u = 0; u < KHM; ++u) {
+    uint4 vh = make_uint4(0, 0, 0, 0), vl = vh;
+    if (u < KH) {
+      const int idx = ((kh * KH + u) * 4 + ct) * 64 + lane;
+      vh = wsh[idx];
+      vl = wsl[idx];
+    }
+    bh[u] = *reinterpret_cast<const f16x8*>(&vh);
+    if (u < NR) bl[u < NR ? u : 0] = *reinterpret_cast<const f16x8*>(&vl);
+    else WL[(wave * LO + (u - NR)) * 64 + lane] = vl;
+  }
+
+  SlotRec n0, n1;
+  SlotRows<KF> d0, d1;
+  // prologue: rows of tile 0 issued, its Z aggregated; rows of tile 1 in flight;
+  // records of tile 2 loading
+  sl_rec(n0, slot(0, r0), num_dst, desc, cols8, lane);
+  sl_rec(n1, slot(0, r1), num_dst, desc, cols8, lane);
+  sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + r0, lane);
+  sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + r1, lane);
+  sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
+  sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
+  if (nv > 0) {
+    sl_store<KF>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                 Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, lane);
+    sl_store<KF>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                 Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, lane);
+  }
+  sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + kTile + r0, lane);
+  sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + kTile + r1, lane);
+  sl_rec(n0, slot(2, r0), num_dst, desc, cols8, lane);
+  sl_rec(n1, slot(2, r1), num_dst, desc, cols8, lane);
+  __syncthreads();
+
+  for (int64_t v = 0; v < nv; ++v) {
+    lane = opaque(threadIdx.x & 63);
+    const int par = int(v & 1);
+    // ---- MFMA: out[16 x 16] of column tile ct over K half kh ----
+    const int aoff = (lane & 15) * ZS + 8 * (lane >> 4) + 32 * kh * KH;
+    const _Float16* ah = Zh + aoff;
+    const _Float16* al = Zl + aoff;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    // A fragments one k-step ahead; the scheduling barriers keep the compiler
+    // from hoisting every LDS read of the tile (registers belong to W)
+    f16x8 nhi = *reinterpret_cast<const f16x8*>(ah);
+    f16x8 nlo = *reinterpret_cast<const f16x8*>(al);
+#pragma unroll
+    for (int u = 0; u < KHM; ++u) {
+      if (u < KH && mode != 1) {
+        const f16x8 ahi = nhi, alo = nlo;
+        if (u + 1 < KH) {
+          nhi = *reinterpret_cast<const f16x8*>(ah + 32 * (u + 1));
+          nlo = *reinterpret_cast<const f16x8*>(al + 32 * (u + 1));
+        }
+        f16x8 blo;
+        if (u < NR) {
+          blo = bl[u < NR ? u : 0];
+        } else {
+          const uint4 w = WL[(wave * LO + (u - NR)) * 64 + lane];
+          blo = *reinterpret_cast<const f16x8*>(&w);
+        }
+        f32x4& acc = (u & 1) ? acc1 : acc0;
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[u], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    acc0 += acc1;
+    if (kh) red[ct * 64 + lane] = acc0;
+    __syncthreads();  // partials visible; every Z read of this tile done
+
+    // ---- reduce + store: waves 0-3, column tile ct ----
+    if (!kh) {
+      const float* rsc = rsc0 + par * kTile;
+      const int* rid = rid0 + par * kTile;
+      const f32x4 sum = acc0 + red[ct * 64 + lane];
+      const int n = ct * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = (lane >> 4) * 4 + q;
+        const int ri = rid[r];
+        if (ri >= 0) out[int64_t(ri) * C + n] = sum[q] * (rsc[r] * wu) + bcol;
+      }
+    }
+
+    // ---- tile v + 1: aggregate its rows into Z; issue tile v + 2, load v + 3 ----
+    if (v + 1 < nv && mode != 2) {
+      const int pn = par ^ 1;
+      sl_store<KF>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+                   stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r0,
+                   lane);
+      sl_store<KF>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+                   stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r1,
+                   lane);
+      sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + par * kTile + r0, lane);
+      sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + par * kTile + r1, lane);
+      sl_rec(n0, slot(v + 3, r0), num_dst, desc, cols8, lane);
+      sl_rec(n1, slot(v + 3, r1), num_dst, desc, cols8, lane);
+    }
+    __syncthreads();  // Z of the next tile complete; reduce reads done
+  }
+}
+
+size_t stream_smem(int Fp, int lo) {
+  return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 4 * 64 +
+         sizeof(SlotRing) * 2 * kTile + sizeof(float) * 4 * kTile +
+         sizeof(uint4) * kSWaves * lo * 64;
+}
+
 // ---------------------------------------------------------------------------
 // Hub chunks: partial (max, sum, unnormalised z) per chunk of a heavy row.
 template <int KF>
@@ -1421,7 +1877,8 @@ int fused_mode() {
   return m;
 }
 
-// GFD_TILE_KERNEL (A/B switch): 0 default (k_fused), 2 persistent weight-stationary,
+// GFD_TILE_KERNEL (A/B switch): 0 default (k_stream where its register budget
+// allows, else k_fused), 1 k_fused, 2 persistent half-stationary (k_persist),
 // 3 32-row tiles, 4 32-row tiles with paired aggregation.
 int tile_kernel() {
   static int m = [] {
@@ -1492,6 +1949,46 @@ gfd_status launch_persist(const AggArgs& a, const PackLayout& L, int64_t tiles,
   return GFD_OK;
 }
 
+template <int KF, int KHM, int LO>
+gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
+                           hipStream_t stream) {
+  auto kern = &k_stream<KF, KHM, LO>;
+  const size_t lds = stream_smem(L.Fp, LO);
+  if (L.KS / 2 > KHM || lds > kLdsBytes || !a.plan.slot_cols) return GFD_ERR_UNSUPPORTED;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsBytes)) !=
+        hipSuccess)
+      return GFD_ERR_HIP;
+    attr_set = true;
+  }
+  int64_t grid = cu_count();
+  if (grid > tiles) grid = tiles;
+  const gfd_plan& p = a.plan;
+  kern<<<int(grid), kSWaves * 64, lds, stream>>>(
+      a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
+      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
+      reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
+      reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
+      reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
+      a.zhub, a.out, a.stats, tiles, fused_mode());
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
+
+// k_stream instance for this K: KH = KS / 2 k-steps per wave, at most KHM = 8 / 16 / 21
+// for one / two / three feature chunks (F <= 64 / 128 / 168); GFD_ERR_UNSUPPORTED
+// beyond (k_fused takes over).  KF = 3 keeps W_lo of 8 k-steps per wave in LDS.
+template <int KF>
+gfd_status launch_stream(const AggArgs& a, const PackLayout& L, int64_t tiles,
+                         hipStream_t stream) {
+  if constexpr (KF == 1) return launch_stream_k<1, 8, 0>(a, L, tiles, stream);
+  else if constexpr (KF == 2) return launch_stream_k<2, 16, 0>(a, L, tiles, stream);
+  else if constexpr (KF == 3) return launch_stream_k<3, 21, 8>(a, L, tiles, stream);
+  return GFD_ERR_UNSUPPORTED;
+}
+
 template <int KF>
 gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
   const int Fp = L.Fp, KP = L.KP;
@@ -1512,6 +2009,10 @@ gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t s
   if (!(a.stages & GFD_STAGE_TILES)) return GFD_OK;
   const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
   if constexpr (KF <= 3) {
+    if (p.slot_desc && tile_kernel() == 0) {
+      gfd_status s = launch_stream<KF>(a, L, tiles, stream);
+      if (s != GFD_ERR_UNSUPPORTED) return s;
+    }
     if (p.slot_desc && tile_kernel() == 2) return launch_persist<KF>(a, L, tiles, stream);
     if (p.slot_desc && (tile_kernel() == 3 || tile_kernel() == 4)) {
       auto kern = tile_kernel() == 4 ? &k_pair<KF> : &k_tile32<KF>;
@@ -1624,6 +2125,10 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   k_pack_frag<<<(n_fr + 255) / 256, 256, 0, stream>>>(weight, F, L.Fp, L.KS, hdr,
                                                       reinterpret_cast<uint4*>(p + L.whi_off),
                                                       reinterpret_cast<uint4*>(p + L.wlo_off));
+  GFD_LAUNCH_CHECK();
+  k_pack_frag_s<<<(n_fr + 255) / 256, 256, 0, stream>>>(weight, F, L.KS, hdr,
+                                                        reinterpret_cast<uint4*>(p + L.wsh_off),
+                                                        reinterpret_cast<uint4*>(p + L.wsl_off));
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
