@@ -101,6 +101,14 @@ def cpu_baseline(args):
                       "dst chunks of 4M messages; 1 warm-up + mean of 2 timed runs"}
 
 
+def tile_kernel_name(F):
+    """The tile-stage kernel gfd_gat_aggregate launches (GFD_TILE_KERNEL, F)."""
+    tk = int(os.environ.get("GFD_TILE_KERNEL", "0"))
+    if tk == 0 and (F + 7) // 8 * 8 <= 168:
+        return "k_stream (weight-stationary tile stage)"
+    return {2: "k_persist", 3: "k_tile32", 4: "k_pair"}.get(tk, "k_fused") + " (tile stage)"
+
+
 def load_pmc(path, workload_key):
     try:
         with open(path) as f:
@@ -212,6 +220,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("GFD_PROF_DUMP") and hasattr(lib, "gfd_debug_prof"):
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        lib.gfd_debug_prof(buf)
+        names = ["mfma", "barrier1", "reduce", "agg0", "agg1", "issue", "barrier2"]
+        tot = sum(buf[:7])
+        log("[bench] k_stream phase cycles (summed over waves): " + ", ".join(
+            f"{n} {buf[i] / max(tot, 1) * 100:.1f}%" for i, n in enumerate(names)) +
+            f"; per tile-wave {tot / max(buf[7], 1):.0f} cyc")
     pre_ms = [e[0].elapsed_time(e[1]) for e in events]
     hub_ms = [e[1].elapsed_time(e[2]) for e in events]
     tile_ms = [e[2].elapsed_time(e[3]) for e in events]
@@ -228,7 +245,8 @@ def main():
     B_layer = M * (s * F + 4) + N * (4 + 4 * C) + 4 * F * H * C
     flop_layer = 2 * N * F * H * C + M * H * (2 * C + 8)
     t_roof = max(B_layer / (HBM_PEAK_GBPS * 1e9), flop_layer / (BF16_PEAK_TFLOPS * 1e12))
-    # dominant kernel = k_fused (tile stage) on this rank: the light messages + all its rows
+    # dominant kernel = the tile stage on this rank (k_stream for F <= 168, else k_fused):
+    # the light messages + all its rows
     hub_msgs = plan.hub_messages()
     light_msgs = m_local - hub_msgs
     B_tile = light_msgs * (s * F + 4) + n_dst * (4 + 4 * C) + 4 * F * H * C
@@ -251,7 +269,7 @@ def main():
                    "hubs": plan.num_hubs, "hub_chunks": plan.num_chunks},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "kernel": "k_fused (tile stage)", "algorithmic_bytes": B_tile,
+                     "kernel": tile_kernel_name(F), "algorithmic_bytes": B_tile,
                      "kernel_ms": t_tile * 1e3},
         "layer": {"algorithmic_bytes": B_layer, "flop": flop_layer,
                   "hbm_gbps": B_layer / (ms_step * 1e-3) / 1e9,

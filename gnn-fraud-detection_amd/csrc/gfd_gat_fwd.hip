@@ -1302,25 +1302,43 @@ __global__ void __launch_bounds__(1024, 4) k_pair(
 
 
 // ---------------------------------------------------------------------------
-// Weight-stationary streaming tile kernel (persistent, one 8-wave block per CU,
-// two waves per SIMD at up to 256 VGPRs).
-//
-//  * The whole projection (fp16 W_hi and W_lo B-fragments, 344 KB at F = 166)
-//    lives in registers for the launch: wave w owns the k-steps
-//    [NM*w, NM*w + NM) for all four column tiles plus NE "extra" units
-//    (k-step 8*NM + (w >> 2) + 2v, column tile w & 3).  Nothing but x rows,
-//    logits and slot records streams from memory per tile.
-//  * Z goes through LDS once per 16-row tile in the feature-major K order
-//    p = 8 f + h, so a lane stores all 8 heads of its feature with one 16-B
-//    write per (hi, lo).  Single accumulator per column tile:
-//    acc += Zhi.Whi + Zhi.Wlo + Zlo.Whi (lo parts unscaled).
-//  * Two destinations per wave (rows 2w, 2w+1); their first batches of x rows
-//    are issued one tile ahead, so they are in flight during the MFMA phase and
-//    the cross-wave reduction of the previous tile.
-//  * Per tile: MFMA -> partials to LDS -> barrier -> reduce + store out (waves
-//    0-3, one column tile each) and aggregate the next tile's rows into Z ->
-//    barrier.
+// k_stream and its slot helpers (kernel comment below).
 constexpr int kSWaves = 8;
+
+#ifdef GFD_CHECKED
+// Checked diagnostic build (-DGFD_CHECKED): every gathered index of k_stream is
+// bounds-checked; the first violation is recorded (site, value, limit, block)
+// and the index replaced by 0, so a bad index reports instead of faulting.
+__device__ long long g_chk[4];
+__device__ long long g_lim[4];  // x/st rows (N), num_dst, num_hubs
+__device__ __noinline__ void chk_fail(int site, long long v, long long lim) {
+  if (atomicCAS(reinterpret_cast<unsigned long long*>(&g_chk[0]), 0ull,
+                (unsigned long long)site) == 0ull) {
+    g_chk[1] = v;
+    g_chk[2] = lim;
+    g_chk[3] = blockIdx.x * 1000 + (threadIdx.x >> 6);
+  }
+}
+#define CHK(site, v, limi) \
+  ((unsigned long long)(v) < (unsigned long long)g_lim[limi] ? (v) : (chk_fail(site, (v), g_lim[limi]), 0))
+#else
+#define CHK(site, v, limi) (v)
+#endif
+
+#ifdef GFD_PROF
+// Phase cycle counters of k_stream (diagnostic builds only, -DGFD_PROF):
+// 0 MFMA, 1 barrier after MFMA, 2 reduce+store, 3 aggregate slot 0,
+// 4 aggregate slot 1, 5 issue+records, 6 barrier after aggregation, 7 tiles
+__device__ unsigned long long g_prof[8];
+#define PROF_MARK(i)                                                              \
+  do {                                                                            \
+    const uint64_t t_ = __builtin_readcyclecounter();                             \
+    if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * 8 + (i)] += t_ - prof_t; \
+    prof_t = t_;                                                                  \
+  } while (0)
+#else
+#define PROF_MARK(i)
+#endif
 
 // The stream kernel's helpers take the lane index as an argument: the kernel
 // launders it (asm) once per tile, so no per-lane address derived from it can
@@ -1360,8 +1378,8 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
                                        const int32_t* __restrict__ cols8, int lane) {
   const int64_t sl = slot < num_dst ? slot : num_dst - 1;
   const int z0 = opaque(0);  // divergent zero: a vector load, not s_load
-  p.d = desc[sl + z0];
-  p.j = cols8[sl * 8 + (lane >> 3)];
+  p.d = desc[CHK(1, sl, 1) + z0];
+  p.j = cols8[CHK(2, sl, 1) * 8 + (lane >> 3)];
   p.live = slot < num_dst;
 }
 
@@ -1379,7 +1397,7 @@ __device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int
   }
 }
 
-// Issue the first batch of a slot (4 rows, t_i, s_j) unconditionally (empty and
+// Issue the first batch of a slot (PF rows, t_i, s_j) unconditionally (empty and
 // hub slots read valid rows that are ignored, so no branch joins in-flight
 // loads) and park the record in the LDS ring for the aggregation.
 template <int KF>
@@ -1389,21 +1407,22 @@ __device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF>& q,
                                          SlotRing* __restrict__ ring, int lane) {
   const int h = lane & 7;
   const int row = __builtin_amdgcn_readfirstlane(p.d.x);  // >= 0: clamped slots are real rows
-  q.th = st[(dst_offset + row) * 16 + H + h];
-  q.sj = st[int64_t(p.j) * 16 + h];
+  q.th = st[CHK(3, dst_offset + row, 0) * 16 + H + h];
+  q.sj = st[int64_t(CHK(4, p.j, 0)) * 16 + h];
 #pragma unroll
   for (int k = 0; k < SlotRows<KF>::PF; ++k) {
     const int jk = __builtin_amdgcn_readlane(p.j, 8 * k);
-    sl_rows<KF>(x + int64_t(jk) * ldx, F, lane, q.xv[k]);
+    sl_rows<KF>(x + int64_t(CHK(5, jk, 0)) * ldx, F, lane, q.xv[k]);
   }
   if (lane == 0) ring->d = make_int4(p.live ? p.d.x : -1, p.d.y, p.d.z, p.d.w);
   if (h == 0) ring->j[lane >> 3] = p.j;
 }
 
+#ifdef GFD_SCALAR_AGG
 // Normalised z of one slot (all 8 heads, lane <-> feature); online softmax over
 // batches of 8 messages, rows in sub-batches of 4; the first sub-batch is in q.
 template <int KF>
-__device__ __forceinline__ void sl_compute(const int4 d, const int j0, const SlotRows<KF>& q,
+__device__ __forceinline__ void sl_compute_s(const int4 d, const int j0, const SlotRows<KF>& q,
                                            const float* __restrict__ x, int64_t ldx, int F,
                                            int Fp, const int32_t* __restrict__ col,
                                            const float* __restrict__ st, float slope, float dp,
@@ -1483,7 +1502,7 @@ __device__ __forceinline__ void sl_compute(const int4 d, const int j0, const Slo
           sl_rows<KF>(x + int64_t(jk) * ldx, F, lane, xl[k]);
         }
       }
-      const int kn = min(4, nk - k0);  // padding rows carry p = 0 anyway
+      const int kn = min(4, nk - k0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (k == 0 || k < kn) {
@@ -1514,9 +1533,6 @@ __device__ __forceinline__ void sl_compute(const int4 d, const int j0, const Slo
   }
 }
 
-// Aggregate one slot (record from the LDS ring, first batch in q) and store its
-// Z row: power-of-two scaled, feature-major (K position 8 f + h), fp16 hi and
-// unscaled lo', one 16-B store per feature each.
 template <int KF>
 __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, const SlotRows<KF>& q,
                                          const float* __restrict__ x, int64_t ldx, int F, int Fp,
@@ -1529,7 +1545,7 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
   const int4 d = uni4(ring->d);
   const int j0 = ring->j[lane >> 3];
   float z[H][KF];
-  sl_compute<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, lane, z);
+  sl_compute_s<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, lane, z);
   float zm = 0.f;
 #pragma unroll
   for (int hh = 0; hh < H; ++hh)
@@ -1563,6 +1579,186 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
     rid[r] = d.x;
   }
 }
+#else
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 bcast2(float v, int l0) {  // (v@l0, v@l0+1), wave-uniform
+  return f32x2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l0)),
+               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l0 + 1))};
+}
+
+// Un-normalised z of one slot, heads in pairs (z2[g] = heads 2g, 2g+1, lane <->
+// feature), and 1 / (sum + eps) of head lane & 7 (1 for hub rows, whose merged
+// z is already normalised).  Online softmax over batches of 8 messages, rows in
+// sub-batches of 4 (the first PF rows prefetched in q); packed FMAs.
+template <int KF>
+__device__ __forceinline__ float sl_compute(const int4 d, const int j0, const SlotRows<KF>& q,
+                                            const float* __restrict__ x, int64_t ldx, int F,
+                                            int Fp, const int32_t* __restrict__ col,
+                                            const float* __restrict__ st, float slope, float dp,
+                                            uint64_t seed, const float* __restrict__ zhub,
+                                            float* __restrict__ stats, int lane,
+                                            f32x2 (&z)[4][KF]) {
+  const int h = lane & 7, kk = lane >> 3;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
+  if (d.x < 0) return 1.0f;
+  if (d.w >= 0) {  // hub: merged row (already normalised)
+    const float* src = zhub + int64_t(CHK(6, d.w, 2)) * (H * Fp);
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq) {
+        const int f = lane + 64 * qq;
+        if (f < Fp) z[g][qq] = f32x2{src[2 * g * Fp + f], src[(2 * g + 1) * Fp + f]};
+      }
+    return 1.0f;
+  }
+  const int e0 = CHK(12, d.y, 3), e1 = CHK(13, d.z, 3);
+  float m = -INFINITY, l = 0.f;
+  for (int b = e0; b < e1; b += 8) {
+    const int e = b + kk;
+    const bool valid = e < e1;
+    int j;
+    float v;
+    if (b == e0) {
+      j = j0;
+      v = leaky(q.sj + q.th, slope);
+    } else {
+      j = col[valid ? e : e1 - 1];
+      v = leaky(st[int64_t(CHK(7, j, 0)) * 16 + h] + q.th, slope);
+    }
+    float bm = valid ? v : -INFINITY;
+    bm = fmaxf(bm, __shfl_xor(bm, 8));
+    bm = fmaxf(bm, __shfl_xor(bm, 16));
+    bm = fmaxf(bm, __shfl_xor(bm, 32));
+    const float mn = fmaxf(m, bm);
+    const float sc = __expf(m - mn);
+    float pv = valid ? __expf(v - mn) : 0.f;
+    l = fmaf(l, sc, pv);
+    if (b != e0 && __any(sc != 1.0f)) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x2 s2 = bcast2(sc, 2 * g);
+#pragma unroll
+        for (int qq = 0; qq < KF; ++qq) z[g][qq] *= s2;
+      }
+    }
+    m = mn;
+    if (dp > 0.f)
+      pv = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? pv * (1.0f / (1.0f - dp)) : 0.f;
+    const int nk = min(8, e1 - b);
+    for (int k0 = 0; k0 < nk; k0 += 4) {
+      float xl[4][KF];
+      constexpr int PF = SlotRows<KF>::PF;
+      if (b == e0 && k0 == 0) {
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+#pragma unroll
+          for (int qq = 0; qq < KF; ++qq) xl[k][qq] = q.xv[k][qq];
+        if (PF < 4 && nk > PF) {
+#pragma unroll
+          for (int k = PF; k < 4; ++k) {
+            const int jk = __builtin_amdgcn_readlane(j, 8 * k);
+            sl_rows<KF>(x + int64_t(CHK(8, jk, 0)) * ldx, F, lane, xl[k]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int jk = __builtin_amdgcn_readlane(j, 8 * (k0 + k));
+          sl_rows<KF>(x + int64_t(CHK(9, jk, 0)) * ldx, F, lane, xl[k]);
+        }
+      }
+      const int kn = min(4, nk - k0);  // padding rows carry p = 0 anyway
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k == 0 || k < kn) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x2 p2 = bcast2(pv, 8 * (k0 + k) + 2 * g);
+#pragma unroll
+            for (int qq = 0; qq < KF; ++qq)
+              z[g][qq] = __builtin_elementwise_fma(p2, f32x2{xl[k][qq], xl[k][qq]}, z[g][qq]);
+          }
+        }
+      }
+    }
+  }
+  l += __shfl_xor(l, 8);
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  if (stats && lane < 8) {
+    stats[int64_t(CHK(11, d.x, 1)) * 16 + lane] = m;
+    stats[int64_t(d.x) * 16 + 8 + lane] = l;
+  }
+  return 1.0f / (l + kSoftmaxEps);
+}
+
+// Aggregate one slot (record from the LDS ring, first batch in q) and store its
+// Z row: normalised, power-of-two scaled (max |z| -> [2^13, 2^14)), feature-major
+// (K position 8 f + h), fp16 hi and unscaled lo', one 16-B store per feature each.
+template <int KF>
+__device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, const SlotRows<KF>& q,
+                                         const float* __restrict__ x, int64_t ldx, int F, int Fp,
+                                         const int32_t* __restrict__ col,
+                                         const float* __restrict__ st, float slope, float dp,
+                                         uint64_t seed, const float* __restrict__ zhub,
+                                         float* __restrict__ stats, _Float16* __restrict__ zh,
+                                         _Float16* __restrict__ zl, float* __restrict__ rsc,
+                                         int* __restrict__ rid, int r, int lane) {
+  const int4 d = uni4(ring->d);
+  const int j0 = ring->j[lane >> 3];
+  f32x2 z[4][KF];
+  const float inv = sl_compute<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+                                   stats, lane, z);
+  float zm = 0.f;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x2 i2 = bcast2(inv, 2 * g);
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) {
+      z[g][qq] *= i2;
+      zm = fmaxf(zm, fmaxf(fabsf(z[g][qq].x), fabsf(z[g][qq].y)));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) zm = fmaxf(zm, __shfl_xor(zm, o));
+  int ex = 0;
+  if (zm > 0.f) frexpf(zm, &ex);
+  int er = 14 - ex;
+  er = er > 100 ? 100 : (er < -100 ? -100 : er);
+  const float rs = ldexpf(1.0f, er);
+  const f32x2 rs2 = {rs, rs};
+#pragma unroll
+  for (int qq = 0; qq < KF; ++qq) {
+    const int f = lane + 64 * qq;
+    if (f < Fp) {
+      union { f16x8 v; _Float16 h[8]; } a, b;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x2 v = z[g][qq] * rs2;
+        const _Float16 h0 = (_Float16)v.x, h1 = (_Float16)v.y;
+        const f32x2 back = {(float)h0, (float)h1};
+        const f32x2 lo = v - back;
+        a.h[2 * g] = h0;
+        a.h[2 * g + 1] = h1;
+        b.h[2 * g] = (_Float16)lo.x;
+        b.h[2 * g + 1] = (_Float16)lo.y;
+      }
+      *reinterpret_cast<f16x8*>(zh + 8 * f) = a.v;
+      *reinterpret_cast<f16x8*>(zl + 8 * f) = b.v;
+    }
+  }
+  if (lane == 0) {
+    rsc[r] = ldexpf(1.0f, -er);
+    rid[r] = d.x;
+  }
+}
+
+#endif  // GFD_SCALAR_AGG
 
 // Weight-stationary streaming tile kernel (persistent, one 8-wave block per CU,
 // two waves per SIMD at up to 256 VGPRs).
@@ -1581,7 +1777,7 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
 //    kernel waits on precedes their use (vmcnt is in order).
 //  * Per tile: MFMA -> kh = 1 partials to LDS -> barrier -> kh = 0 waves reduce
 //    and store out; every wave aggregates its next rows into Z -> barrier.
-template <int KF, int KHM, int LO>
+template <int KF, int KHM, int LO, bool EXACT>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
@@ -1592,7 +1788,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     float* __restrict__ stats, int64_t num_tiles, int mode) {
   extern __shared__ __attribute__((aligned(16))) char ssm[];
   const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
-  const int KH = Fp / 8;                                        // k-steps per K half (<= KHM)
+  const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
   _Float16* Zh = reinterpret_cast<_Float16*>(ssm);              // [16][ZS]
   _Float16* Zl = Zh + kTile * ZS;                               // [16][ZS]
   f32x4* red = reinterpret_cast<f32x4*>(Zl + kTile * ZS);       // [4 ct][64]
@@ -1652,6 +1848,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   sl_rec(n1, slot(2, r1), num_dst, desc, cols8, lane);
   __syncthreads();
 
+#ifdef GFD_PROF
+  __shared__ uint64_t prof_lds[kSWaves * 8];
+  if (lane < 8) prof_lds[wave * 8 + lane] = 0;
+  uint64_t prof_t = __builtin_readcyclecounter();
+#endif
   for (int64_t v = 0; v < nv; ++v) {
     lane = opaque(threadIdx.x & 63);
     const int par = int(v & 1);
@@ -1688,7 +1889,9 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     }
     acc0 += acc1;
     if (kh) red[ct * 64 + lane] = acc0;
+    PROF_MARK(0);
     __syncthreads();  // partials visible; every Z read of this tile done
+    PROF_MARK(1);
 
     // ---- reduce + store: waves 0-3, column tile ct ----
     if (!kh) {
@@ -1700,26 +1903,37 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       for (int q = 0; q < 4; ++q) {
         const int r = (lane >> 4) * 4 + q;
         const int ri = rid[r];
-        if (ri >= 0) out[int64_t(ri) * C + n] = sum[q] * (rsc[r] * wu) + bcol;
+        if (ri >= 0) out[int64_t(CHK(10, ri, 1)) * C + n] = sum[q] * (rsc[r] * wu) + bcol;
       }
     }
 
     // ---- tile v + 1: aggregate its rows into Z; issue tile v + 2, load v + 3 ----
+    PROF_MARK(2);
     if (v + 1 < nv && mode != 2) {
       const int pn = par ^ 1;
       sl_store<KF>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                    stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r0,
                    lane);
+      PROF_MARK(3);
       sl_store<KF>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                    stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r1,
                    lane);
+      PROF_MARK(4);
       sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + par * kTile + r0, lane);
       sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + par * kTile + r1, lane);
       sl_rec(n0, slot(v + 3, r0), num_dst, desc, cols8, lane);
       sl_rec(n1, slot(v + 3, r1), num_dst, desc, cols8, lane);
+      PROF_MARK(5);
     }
     __syncthreads();  // Z of the next tile complete; reduce reads done
+    PROF_MARK(6);
+#ifdef GFD_PROF
+    if (lane == 0) prof_lds[wave * 8 + 7] += 1;
+#endif
   }
+#ifdef GFD_PROF
+  if (lane < 8) atomicAdd(&g_prof[lane], (unsigned long long)prof_lds[wave * 8 + lane]);
+#endif
 }
 
 size_t stream_smem(int Fp, int lo) {
@@ -1901,6 +2115,7 @@ int cu_count() {
 
 struct AggArgs {
   const float* x; int F; int64_t ldx;
+  int64_t N;  // rows of x / st (checked builds only)
   const int32_t* rowptr; const int32_t* col; int64_t num_dst; int64_t dst_offset;
   const float* st; const char* packed; const float* bias; float slope; float dp; uint64_t seed;
   gfd_plan plan; int stages; float* out; float* stats;
@@ -1949,23 +2164,31 @@ gfd_status launch_persist(const AggArgs& a, const PackLayout& L, int64_t tiles,
   return GFD_OK;
 }
 
-template <int KF, int KHM, int LO>
+template <int KF, int KHM, int LO, bool EXACT>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
                            hipStream_t stream) {
-  auto kern = &k_stream<KF, KHM, LO>;
+  auto kern = &k_stream<KF, KHM, LO, EXACT>;
+  if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
   const size_t lds = stream_smem(L.Fp, LO);
   if (L.KS / 2 > KHM || lds > kLdsBytes || !a.plan.slot_cols) return GFD_ERR_UNSUPPORTED;
-  static bool attr_set = false;
-  if (!attr_set) {
+  static size_t attr_lds = 0;  // dynamic LDS the attribute currently allows
+  if (lds > attr_lds) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kLdsBytes)) !=
-        hipSuccess)
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)) != hipSuccess)
       return GFD_ERR_HIP;
-    attr_set = true;
+    attr_lds = lds;
   }
   int64_t grid = cu_count();
   if (grid > tiles) grid = tiles;
   const gfd_plan& p = a.plan;
+#ifdef GFD_CHECKED
+  {
+    const long long lim[4] = {a.N, a.num_dst, a.plan.num_hubs, 1ll << 31};
+    if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lim), lim, sizeof(lim), 0, hipMemcpyHostToDevice,
+                               stream) != hipSuccess)
+      return GFD_ERR_HIP;
+  }
+#endif
   kern<<<int(grid), kSWaves * 64, lds, stream>>>(
       a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
       reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
@@ -1983,9 +2206,17 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
 template <int KF>
 gfd_status launch_stream(const AggArgs& a, const PackLayout& L, int64_t tiles,
                          hipStream_t stream) {
-  if constexpr (KF == 1) return launch_stream_k<1, 8, 0>(a, L, tiles, stream);
-  else if constexpr (KF == 2) return launch_stream_k<2, 16, 0>(a, L, tiles, stream);
-  else if constexpr (KF == 3) return launch_stream_k<3, 21, 8>(a, L, tiles, stream);
+  const bool exact = L.KS / 2 == (KF == 1 ? 8 : KF == 2 ? 16 : 21);
+  if constexpr (KF == 1) {
+    return exact ? launch_stream_k<1, 8, 0, true>(a, L, tiles, stream)
+                 : launch_stream_k<1, 8, 0, false>(a, L, tiles, stream);
+  } else if constexpr (KF == 2) {
+    return exact ? launch_stream_k<2, 16, 0, true>(a, L, tiles, stream)
+                 : launch_stream_k<2, 16, 0, false>(a, L, tiles, stream);
+  } else if constexpr (KF == 3) {
+    return exact ? launch_stream_k<3, 21, 8, true>(a, L, tiles, stream)
+                 : launch_stream_k<3, 21, 8, false>(a, L, tiles, stream);
+  }
   return GFD_ERR_UNSUPPORTED;
 }
 
@@ -2101,6 +2332,27 @@ size_t hub_ws_layout(Carve* c, int64_t num_hubs, int64_t num_chunks, const PackL
 
 extern "C" {
 
+#ifdef GFD_CHECKED
+// checked builds: first bounds violation {site, value, limit, block*1000+wave}; reset after read
+int gfd_debug_chk(long long* host4) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host4, HIP_SYMBOL(g_chk), sizeof(long long) * 4) != hipSuccess) return -1;
+  long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_chk), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef GFD_PROF
+// diagnostic builds: k_stream phase cycles summed over waves (see g_prof); reset after read
+int gfd_debug_prof(unsigned long long* host8) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -1;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 size_t gfd_gat_packed_size(int in_features, int heads, int channels) {
   if (!check_hc(heads, channels, in_features)) return 0;
   return pack_layout(in_features).bytes;
@@ -2171,7 +2423,7 @@ gfd_status gfd_gat_aggregate(const float* x, int64_t N, int F, int64_t ldx, cons
   if (!st || !packed || stages < 1 || stages > 3) return GFD_ERR_ARGUMENT;
   if (num_dst == 0) return GFD_OK;
   PackLayout L = pack_layout(F);
-  AggArgs a{x, F, ldx, rowptr, col, num_dst, dst_offset, st, static_cast<const char*>(packed),
+  AggArgs a{x, F, ldx, N, rowptr, col, num_dst, dst_offset, st, static_cast<const char*>(packed),
             bias, slope, dp, seed, p, stages, out, stats, nullptr, nullptr, nullptr};
   if (p.num_hubs > 0) {
     Carve c(ws, ws_bytes);
@@ -2196,7 +2448,7 @@ gfd_status gfd_gat_fwd(const float* x, int64_t N, int F, int64_t ldx, const int3
     return GFD_ERR_WORKSPACE;
   PackLayout L = pack_layout(F);
   Carve c(ws, ws_bytes);
-  AggArgs a{x, F, ldx, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p, GFD_STAGE_ALL,
+  AggArgs a{x, F, ldx, N, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p, GFD_STAGE_ALL,
             out, stats, nullptr, nullptr, nullptr};
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.hubstat, &a.zhub);
   void* packed = c.take<char>(L.bytes);

@@ -12,7 +12,9 @@ import threading
 
 _LIB = None
 _LOCK = threading.Lock()
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgfd.so")
+# GFD_LIB_PATH: an alternative build of the same ABI (e.g. the -DGFD_PROF diagnostic build)
+LIB_PATH = os.environ.get("GFD_LIB_PATH") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libgfd.so")
 
 c_i32, c_i64, c_u64, c_f32, c_sz = ct.c_int32, ct.c_int64, ct.c_uint64, ct.c_float, ct.c_size_t
 P = ct.c_void_p

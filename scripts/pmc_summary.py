@@ -44,7 +44,7 @@ def main():
         wb = write[k] * 1024
         kernels[k] = {"fetch_size_kib_raw": fetch[k], "fetch_bytes": fb, "write_bytes": wb,
                       "hbm_bytes_per_launch": fb + wb}
-    tile = next((k for k in kernels if k.startswith("k_fused") or k.startswith("k_persist")), None)
+    tile = next((k for k in kernels if k.startswith(("k_stream", "k_fused", "k_persist"))), None)
     entry = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (two passes) {tag}",
              "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 128-B requests at 64 B)",
              "kernels": kernels}
