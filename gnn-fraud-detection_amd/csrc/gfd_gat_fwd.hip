@@ -1580,6 +1580,36 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
   }
 }
 #else
+// In-register cross-lane reductions (DPP row rotate + gfx950 permlane swaps):
+// a few VALU cycles each instead of a ds_bpermute round trip through the LDS
+// unit per step (__shfl_xor).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float max_xor16_32(float v) {  // over lanes xor 16, 32
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float max_xor8_16_32(float v) {  // same head (lane & 7), all messages
+  return max_xor16_32(fmaxf(v, dpp_mov<0x128>(v)));        // row_ror:8
+}
+__device__ __forceinline__ float sum_xor8_16_32(float v) {
+  v += dpp_mov<0x128>(v);
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ float max_wave(float v) {  // all 64 lanes
+  v = fmaxf(v, dpp_mov<0x121>(v));  // row_ror:1
+  v = fmaxf(v, dpp_mov<0x122>(v));  // row_ror:2
+  v = fmaxf(v, dpp_mov<0x124>(v));  // row_ror:4
+  return max_xor8_16_32(v);
+}
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x2 bcast2(float v, int l0) {  // (v@l0, v@l0+1), wave-uniform
@@ -1630,10 +1660,7 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
       j = col[valid ? e : e1 - 1];
       v = leaky(st[int64_t(CHK(7, j, 0)) * 16 + h] + q.th, slope);
     }
-    float bm = valid ? v : -INFINITY;
-    bm = fmaxf(bm, __shfl_xor(bm, 8));
-    bm = fmaxf(bm, __shfl_xor(bm, 16));
-    bm = fmaxf(bm, __shfl_xor(bm, 32));
+    const float bm = max_xor8_16_32(valid ? v : -INFINITY);
     const float mn = fmaxf(m, bm);
     const float sc = __expf(m - mn);
     float pv = valid ? __expf(v - mn) : 0.f;
@@ -1687,9 +1714,7 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
       }
     }
   }
-  l += __shfl_xor(l, 8);
-  l += __shfl_xor(l, 16);
-  l += __shfl_xor(l, 32);
+  l = sum_xor8_16_32(l);
   if (stats && lane < 8) {
     stats[int64_t(CHK(11, d.x, 1)) * 16 + lane] = m;
     stats[int64_t(d.x) * 16 + 8 + lane] = l;
@@ -1724,8 +1749,7 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
       zm = fmaxf(zm, fmaxf(fabsf(z[g][qq].x), fabsf(z[g][qq].y)));
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) zm = fmaxf(zm, __shfl_xor(zm, o));
+  zm = max_wave(zm);
   int ex = 0;
   if (zm > 0.f) frexpf(zm, &ex);
   int er = 14 - ex;
