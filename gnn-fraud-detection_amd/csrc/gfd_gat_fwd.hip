@@ -202,6 +202,59 @@ __global__ void __launch_bounds__(256) k_logits(const float* __restrict__ x, int
   }
 }
 
+// Same product with the logit vectors stationary in registers (KSM k-steps of
+// 16 features, 4 * KSM VGPRs) and all KSM x loads of a 16-row tile issued
+// before the first MFMA: one 16-B load per lane and k-step streams from HBM,
+// nothing else.  Rows 16-B aligned (ldx % 4 == 0, x 16-B aligned).
+template <int KSM>
+__global__ void __launch_bounds__(256) k_logits_s(const float* __restrict__ x, int64_t rows,
+                                                  int F, int64_t ldx,
+                                                  const float* __restrict__ uv, int Fu,
+                                                  float* __restrict__ st) {
+  const int lane = threadIdx.x & 63;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t wave = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  const int64_t nwave = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const int64_t tiles = (rows + 15) / 16;
+  const int ksf = F / 16;                       // k-steps fully inside the row
+  const int kst = (F + 15) / 16;                // including the ragged tail
+  f32x4 b[KSM];
+#pragma unroll
+  for (int s = 0; s < KSM; ++s)
+    b[s] = s < kst ? *reinterpret_cast<const f32x4*>(uv + rl * Fu + 16 * s + 4 * g)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t t = wave; t < tiles; t += nwave) {
+    const int64_t row = t * 16 + rl;
+    const float* xr = x + (row < rows ? row : rows - 1) * ldx + 4 * g;
+    f32x4 a[KSM];
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) {
+      if (s < ksf) {
+        a[s] = *reinterpret_cast<const f32x4*>(xr + 16 * s);
+      } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int f = 16 * s + 4 * g + u;
+          a[s][u] = f < F ? xr[16 * s + u] : 0.f;
+        }
+      } else {
+        a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KSM; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (s < kst) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][u], b[s][u], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t orow = t * 16 + 4 * g + r;
+      if (orow < rows) st[orow * 16 + rl] = acc[r];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // One destination segment (or hub chunk) on one wave, single pass with an
 // online softmax.  Logit lane layout: lane = 8*k + h (message k of a batch of
@@ -2077,13 +2130,24 @@ size_t fused_smem(int Fp) {  // fp16 hi + lo half-tile (= 4 B per element) + par
   return sizeof(float) * (kTile * (4 * Fp + 8) + 3 * 4 * 64 * 4 + 2 * kTile);
 }
 
+int cu_count();
+
 gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const float* uv, int Fu,
                          float* st, hipStream_t stream) {
   if (rows <= 0) return GFD_OK;
   int64_t blocks = (rows + 63) / 64;  // 4 waves x 16 rows
   if (blocks > 8192) blocks = 8192;
   const uintptr_t a = reinterpret_cast<uintptr_t>(x);
-  if (a % 16 == 0 && ldx % 4 == 0)
+  if (a % 16 == 0 && ldx % 4 == 0 && F <= 256) {
+    const int64_t tiles = (rows + 15) / 16;
+    int64_t nb = (tiles + 3) / 4;
+    const int64_t cap = int64_t(cu_count()) * 8;  // resident blocks; grid-stride beyond
+    if (nb > cap) nb = cap;
+    if (F <= 176)
+      k_logits_s<11><<<int(nb), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
+    else
+      k_logits_s<16><<<int(nb), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
+  } else if (a % 16 == 0 && ldx % 4 == 0)
     k_logits<4><<<int(blocks), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
   else if (a % 8 == 0 && ldx % 2 == 0)
     k_logits<2><<<int(blocks), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
