@@ -222,12 +222,13 @@ def main():
     elapsed = time.perf_counter() - t0
     if os.environ.get("GFD_PROF_DUMP") and hasattr(lib, "gfd_debug_prof"):
         import ctypes
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 16)()
         lib.gfd_debug_prof(buf)
-        names = ["mfma", "barrier1", "reduce", "agg0", "agg1", "issue", "barrier2"]
-        tot = sum(buf[:7])
+        names = {0: "mfma", 1: "barrier1", 2: "reduce", 8: "wait-rows", 3: "agg0", 4: "agg1",
+                 5: "issue", 6: "barrier2"}
+        tot = sum(buf[i] for i in names)
         log("[bench] k_stream phase cycles (summed over waves): " + ", ".join(
-            f"{n} {buf[i] / max(tot, 1) * 100:.1f}%" for i, n in enumerate(names)) +
+            f"{n} {buf[i] / max(tot, 1) * 100:.1f}%" for i, n in names.items()) +
             f"; per tile-wave {tot / max(buf[7], 1):.0f} cyc")
     pre_ms = [e[0].elapsed_time(e[1]) for e in events]
     hub_ms = [e[1].elapsed_time(e[2]) for e in events]

@@ -1382,11 +1382,11 @@ __device__ __noinline__ void chk_fail(int site, long long v, long long lim) {
 // Phase cycle counters of k_stream (diagnostic builds only, -DGFD_PROF):
 // 0 MFMA, 1 barrier after MFMA, 2 reduce+store, 3 aggregate slot 0,
 // 4 aggregate slot 1, 5 issue+records, 6 barrier after aggregation, 7 tiles
-__device__ unsigned long long g_prof[8];
+__device__ unsigned long long g_prof[16];
 #define PROF_MARK(i)                                                              \
   do {                                                                            \
     const uint64_t t_ = __builtin_readcyclecounter();                             \
-    if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * 8 + (i)] += t_ - prof_t; \
+    if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * 16 + (i)] += t_ - prof_t; \
     prof_t = t_;                                                                  \
   } while (0)
 #else
@@ -1420,7 +1420,7 @@ struct SlotRing {  // the same record parked in LDS between issue and aggregatio
 
 template <int KF>
 struct SlotRows {  // first batch in flight
-  static constexpr int PF = KF >= 3 ? 2 : 4;  // rows issued ahead (register budget)
+  static constexpr int PF = KF >= 3 ? 4 : 4;  // rows issued ahead (register budget)
   float th;        // t_i of head lane & 7
   float sj;        // s_j of the lane's message
   float xv[PF][KF];  // x rows of messages 0..PF-1 (lane <-> feature)
@@ -1443,11 +1443,14 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
 template <int KF>
 __device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int lane,
                                         float (&v)[KF]) {
+  // a buffer descriptor per (wave-uniform) row: 32-bit lane offsets with the
+  // q * 256 B steps folded into the instruction, and the hardware range check
+  // returns 0 for lanes f >= F -- no per-lane address arithmetic, no clamping
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xr), 0, F * 4, 0x00020000);
 #pragma unroll
-  for (int q = 0; q < KF; ++q) {
-    const int f = lane + 64 * q;
-    v[q] = xr[f < F ? f : F - 1];
-  }
+  for (int q = 0; q < KF; ++q)
+    v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (lane + 64 * q) * 4, 0, 0));
 }
 
 // Issue the first batch of a slot (PF rows, t_i, s_j) unconditionally (empty and
@@ -1664,6 +1667,7 @@ __device__ __forceinline__ float max_wave(float v) {  // all 64 lanes
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x2 bcast2(float v, int l0) {  // (v@l0, v@l0+1), wave-uniform
   return f32x2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l0)),
@@ -1813,17 +1817,13 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
   for (int qq = 0; qq < KF; ++qq) {
     const int f = lane + 64 * qq;
     if (f < Fp) {
-      union { f16x8 v; _Float16 h[8]; } a, b;
+      union { f16x8 v; f16x2 p[4]; } a, b;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < 4; ++g) {  // per head pair: cvt_pk, 2 cvt back, pk_add, cvt_pk
         const f32x2 v = z[g][qq] * rs2;
-        const _Float16 h0 = (_Float16)v.x, h1 = (_Float16)v.y;
-        const f32x2 back = {(float)h0, (float)h1};
-        const f32x2 lo = v - back;
-        a.h[2 * g] = h0;
-        a.h[2 * g + 1] = h1;
-        b.h[2 * g] = (_Float16)lo.x;
-        b.h[2 * g + 1] = (_Float16)lo.y;
+        const f16x2 hv = __builtin_convertvector(v, f16x2);
+        a.p[g] = hv;
+        b.p[g] = __builtin_convertvector(v - __builtin_convertvector(hv, f32x2), f16x2);
       }
       *reinterpret_cast<f16x8*>(zh + 8 * f) = a.v;
       *reinterpret_cast<f16x8*>(zl + 8 * f) = b.v;
@@ -1926,8 +1926,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   __syncthreads();
 
 #ifdef GFD_PROF
-  __shared__ uint64_t prof_lds[kSWaves * 8];
-  if (lane < 8) prof_lds[wave * 8 + lane] = 0;
+  __shared__ uint64_t prof_lds[kSWaves * 16];
+  if (lane < 16) prof_lds[wave * 16 + lane] = 0;
   uint64_t prof_t = __builtin_readcyclecounter();
 #endif
   for (int64_t v = 0; v < nv; ++v) {
@@ -1988,6 +1988,10 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     PROF_MARK(2);
     if (v + 1 < nv && mode != 2) {
       const int pn = par ^ 1;
+#ifdef GFD_PROF_WAIT  // diagnostic: time the wait for the prefetched rows separately
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PROF_MARK(8);
+#endif
       sl_store<KF>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                    stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r0,
                    lane);
@@ -2005,11 +2009,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     __syncthreads();  // Z of the next tile complete; reduce reads done
     PROF_MARK(6);
 #ifdef GFD_PROF
-    if (lane == 0) prof_lds[wave * 8 + 7] += 1;
+    if (lane == 0) prof_lds[wave * 16 + 7] += 1;
 #endif
   }
 #ifdef GFD_PROF
-  if (lane < 8) atomicAdd(&g_prof[lane], (unsigned long long)prof_lds[wave * 8 + lane]);
+  if (lane < 16) atomicAdd(&g_prof[lane], (unsigned long long)prof_lds[wave * 16 + lane]);
 #endif
 }
 
@@ -2432,11 +2436,11 @@ int gfd_debug_chk(long long* host4) {
 
 #ifdef GFD_PROF
 // diagnostic builds: k_stream phase cycles summed over waves (see g_prof); reset after read
-int gfd_debug_prof(unsigned long long* host8) {
+int gfd_debug_prof(unsigned long long* host16) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 8) != hipSuccess)
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) != hipSuccess)
     return -1;
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long z[16] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

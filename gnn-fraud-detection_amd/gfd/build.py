@@ -33,6 +33,8 @@ if VARIANT == "scalar":
     FLAGS.append("-DGFD_SCALAR_AGG")
 elif VARIANT == "prof":
     FLAGS.append("-DGFD_PROF")
+elif VARIANT == "profw":  # prof + a separate wait for the prefetched rows
+    FLAGS += ["-DGFD_PROF", "-DGFD_PROF_WAIT"]
 elif VARIANT == "chk":   # bounds-checked k_stream (reports the first bad index instead of faulting)
     FLAGS.append("-DGFD_CHECKED")
 
