@@ -1357,6 +1357,13 @@ __global__ void __launch_bounds__(1024, 4) k_pair(
 // ---------------------------------------------------------------------------
 // k_stream and its slot helpers (kernel comment below).
 constexpr int kSWaves = 8;
+// k_stream phase ablation for diagnostic builds (-DGFD_STREAM_ABLATE=1: no MFMA,
+// 2: no aggregation); compile-time so the product kernel carries no branch
+#ifdef GFD_STREAM_ABLATE
+constexpr int kAblate = GFD_STREAM_ABLATE;
+#else
+constexpr int kAblate = 0;
+#endif
 
 #ifdef GFD_CHECKED
 // Checked diagnostic build (-DGFD_CHECKED): every gathered index of k_stream is
@@ -1734,7 +1741,9 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
     if (dp > 0.f)
       pv = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? pv * (1.0f / (1.0f - dp)) : 0.f;
     const int nk = min(8, e1 - b);
-    for (int k0 = 0; k0 < nk; k0 += 4) {
+#pragma unroll
+    for (int k0 = 0; k0 < 8; k0 += 4) {  // unrolled: constant readlane lanes
+      if (k0 >= nk) break;
       float xl[4][KF];
       constexpr int PF = SlotRows<KF>::PF;
       if (b == e0 && k0 == 0) {
@@ -1938,24 +1947,32 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const _Float16* ah = Zh + aoff;
     const _Float16* al = Zl + aoff;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    // A fragments one k-step ahead; the scheduling barriers keep the compiler
-    // from hoisting every LDS read of the tile (registers belong to W)
-    f16x8 nhi = *reinterpret_cast<const f16x8*>(ah);
-    f16x8 nlo = *reinterpret_cast<const f16x8*>(al);
+    // A fragments (and LDS-resident W_lo) AP k-steps ahead; the scheduling
+    // barriers keep the compiler from hoisting every LDS read of the tile
+    // (registers belong to W)
+    constexpr int AP = 2;
+    f16x8 phi[AP], plo[AP], pwl[AP];
+#pragma unroll
+    for (int u = 0; u < AP; ++u) {
+      phi[u] = *reinterpret_cast<const f16x8*>(ah + 32 * u);
+      plo[u] = *reinterpret_cast<const f16x8*>(al + 32 * u);
+      if (u >= NR) {
+        const uint4 w = WL[(wave * LO + (u - NR)) * 64 + lane];
+        pwl[u] = *reinterpret_cast<const f16x8*>(&w);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < KHM; ++u) {
-      if (u < KH && mode != 1) {
-        const f16x8 ahi = nhi, alo = nlo;
-        if (u + 1 < KH) {
-          nhi = *reinterpret_cast<const f16x8*>(ah + 32 * (u + 1));
-          nlo = *reinterpret_cast<const f16x8*>(al + 32 * (u + 1));
-        }
-        f16x8 blo;
-        if (u < NR) {
-          blo = bl[u < NR ? u : 0];
-        } else {
-          const uint4 w = WL[(wave * LO + (u - NR)) * 64 + lane];
-          blo = *reinterpret_cast<const f16x8*>(&w);
+      if (u < KH && kAblate != 1) {
+        const f16x8 ahi = phi[u % AP], alo = plo[u % AP];
+        f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % AP];
+        if (u + AP < KH) {
+          phi[u % AP] = *reinterpret_cast<const f16x8*>(ah + 32 * (u + AP));
+          plo[u % AP] = *reinterpret_cast<const f16x8*>(al + 32 * (u + AP));
+          if (u + AP >= NR) {
+            const uint4 w = WL[(wave * LO + (u + AP - NR)) * 64 + lane];
+            pwl[u % AP] = *reinterpret_cast<const f16x8*>(&w);
+          }
         }
         f32x4& acc = (u & 1) ? acc1 : acc0;
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
@@ -1986,7 +2003,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 
     // ---- tile v + 1: aggregate its rows into Z; issue tile v + 2, load v + 3 ----
     PROF_MARK(2);
-    if (v + 1 < nv && mode != 2) {
+    if (v + 1 < nv && kAblate != 2) {
       const int pn = par ^ 1;
 #ifdef GFD_PROF_WAIT  // diagnostic: time the wait for the prefetched rows separately
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
