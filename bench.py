@@ -224,8 +224,8 @@ def main():
         import ctypes
         buf = (ctypes.c_ulonglong * 16)()
         lib.gfd_debug_prof(buf)
-        names = {0: "mfma", 1: "barrier1", 2: "reduce", 8: "wait-rows", 3: "agg0", 4: "agg1",
-                 5: "issue", 6: "barrier2"}
+        names = {0: "mfma", 1: "barrier1", 2: "reduce", 8: "wait-rows", 9: "agg-compute",
+                 3: "agg-epilogue0", 4: "agg-epilogue1", 5: "issue", 6: "barrier2"}
         tot = sum(buf[i] for i in names)
         log("[bench] k_stream phase cycles (summed over waves): " + ", ".join(
             f"{n} {buf[i] / max(tot, 1) * 100:.1f}%" for i, n in names.items()) +

@@ -1396,8 +1396,12 @@ __device__ unsigned long long g_prof[16];
     if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * 16 + (i)] += t_ - prof_t; \
     prof_t = t_;                                                                  \
   } while (0)
+#define PROF_PARAMS , uint64_t &prof_t, uint64_t *prof_lds
+#define PROF_PASS , prof_t, prof_lds
 #else
 #define PROF_MARK(i)
+#define PROF_PARAMS
+#define PROF_PASS
 #endif
 
 // The stream kernel's helpers take the lane index as an argument: the kernel
@@ -1799,12 +1803,13 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
                                          uint64_t seed, const float* __restrict__ zhub,
                                          float* __restrict__ stats, _Float16* __restrict__ zh,
                                          _Float16* __restrict__ zl, float* __restrict__ rsc,
-                                         int* __restrict__ rid, int r, int lane) {
+                                         int* __restrict__ rid, int r, int lane PROF_PARAMS) {
   const int4 d = uni4(ring->d);
   const int j0 = ring->j[lane >> 3];
   f32x2 z[4][KF];
   const float inv = sl_compute<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                                    stats, lane, z);
+  PROF_MARK(9);
   float zm = 0.f;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1912,6 +1917,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     else WL[(wave * LO + (u - NR)) * 64 + lane] = vl;
   }
 
+#ifdef GFD_PROF
+  __shared__ uint64_t prof_lds[kSWaves * 16];
+  if (lane < 16) prof_lds[wave * 16 + lane] = 0;
+  uint64_t prof_t = __builtin_readcyclecounter();
+#endif
   SlotRec n0, n1;
   SlotRows<KF> d0, d1;
   // prologue: rows of tile 0 issued, its Z aggregated; rows of tile 1 in flight;
@@ -1924,9 +1934,9 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
   if (nv > 0) {
     sl_store<KF>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
-                 Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, lane);
+                 Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, lane PROF_PASS);
     sl_store<KF>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
-                 Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, lane);
+                 Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, lane PROF_PASS);
   }
   sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + kTile + r0, lane);
   sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + kTile + r1, lane);
@@ -1934,11 +1944,6 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   sl_rec(n1, slot(2, r1), num_dst, desc, cols8, lane);
   __syncthreads();
 
-#ifdef GFD_PROF
-  __shared__ uint64_t prof_lds[kSWaves * 16];
-  if (lane < 16) prof_lds[wave * 16 + lane] = 0;
-  uint64_t prof_t = __builtin_readcyclecounter();
-#endif
   for (int64_t v = 0; v < nv; ++v) {
     lane = opaque(threadIdx.x & 63);
     const int par = int(v & 1);
@@ -2011,11 +2016,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #endif
       sl_store<KF>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                    stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r0,
-                   lane);
+                   lane PROF_PASS);
       PROF_MARK(3);
       sl_store<KF>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                    stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r1,
-                   lane);
+                   lane PROF_PASS);
       PROF_MARK(4);
       sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + par * kTile + r0, lane);
       sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + par * kTile + r1, lane);

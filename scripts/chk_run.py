@@ -19,7 +19,9 @@ def chk(tag):
     print(f"{tag}: site={buf[0]} value={buf[1]} limit={buf[2]} block*1000+wave={buf[3]}", flush=True)
 dev = torch.device("cuda", 0)
 H, C = 8, 64
-for (N, E, F, world) in [(20000, 160000, 166, 2), (20000, 160000, 166, 1), (3000, 3450, 166, 1)]:
+for (N, E, F, world) in [(20000, 160000, 166, 2), (20000, 160000, 166, 1), (3000, 3450, 166, 1),
+                         (20000, 160000, 128, 2), (20000, 160000, 100, 1), (20000, 160000, 64, 3),
+                         (20000, 160000, 17, 1)]:
     g = torch.Generator().manual_seed(11)
     ei = torch.from_numpy(synth.power_law(N, E, gamma=2.1, seed=11))
     x = torch.randn(N, F, generator=g)

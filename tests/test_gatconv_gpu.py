@@ -90,6 +90,13 @@ def _random_case(N, E, F, seed, kind="powerlaw"):
     (2000, 8000, 166, "powerlaw"),  # BASELINE width
     (500, 3000, 200, "powerlaw"),
     (333, 4000, 256, "powerlaw"),   # max width
+    # k_stream's three register layouts (1, 2, 3 feature chunks) over many tiles per
+    # block (N / 16 tiles on 256 blocks: the row/record pipeline runs several laps),
+    # exact (F = 64, 128, 166) and padded (F = 100) K halves
+    (20000, 160000, 64, "powerlaw"),
+    (20000, 160000, 100, "powerlaw"),
+    (20000, 160000, 128, "powerlaw"),
+    (20000, 160000, 166, "powerlaw"),
 ])
 def test_forward_vs_oracle(N, E, F, kind):
     gnn, _ = _gfd()
