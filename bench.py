@@ -13,8 +13,8 @@ softmax-aggregate-project tiles, inputs already resident in HBM.
 
 value = input edges of the whole graph per second (all ranks together); the
 timed region is bracketed by barrier + synchronize, max over ranks.
-Rank 0 prints ONE JSON line with ``roofline`` (dominant kernel: the fused tile
-kernel ``k_fused``, timed live with HIP events on the launch stream) and
+Rank 0 prints ONE JSON line with ``roofline`` (dominant kernel: the tile stage,
+``k_stream`` for F <= 168, timed live with HIP events on the launch stream) and
 ``cpu_baseline`` (the oracle's PyG-dataflow restatement on a bounded sample,
 host cores of the same box, N=1 only).
 """
@@ -255,7 +255,7 @@ def main():
     achieved = B_tile / t_tile / 1e9
     workload = (f"C4 power-law N={N} E={E} F={F} gamma={args.gamma}: GATConv layer-0 forward "
                 f"(H=8, C=64, concat=False, self loops)")
-    pmc = load_pmc(args.pmc, f"k_fused:N={N}:E={E}:F={F}:world={world}")
+    pmc = load_pmc(args.pmc, f"tile:N={N}:E={E}:F={F}:world={world}")
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
 
     res = {

@@ -51,7 +51,7 @@ def main():
     if tile:
         entry["tile_kernel"] = tile
         entry["hbm_bytes_per_launch"] = kernels[tile]["hbm_bytes_per_launch"]
-    summary[f"k_fused:N={N}:E={E}:F={F}:world={world}"] = entry
+    summary[f"tile:N={N}:E={E}:F={F}:world={world}"] = entry
     json.dump(summary, open(out_path, "w"), indent=1, sort_keys=True)
     for k, v in kernels.items():
         print(f"{k:28s} fetch {v['fetch_bytes'] / 1e9:8.3f} GB  write {v['write_bytes'] / 1e9:8.3f} GB")
