@@ -230,6 +230,9 @@ def main():
         log("[bench] k_stream phase cycles (summed over waves): " + ", ".join(
             f"{n} {buf[i] / max(tot, 1) * 100:.1f}%" for i, n in names.items()) +
             f"; per tile-wave {tot / max(buf[7], 1):.0f} cyc")
+        log("[bench] k_stream slot cycles by degree: " + ", ".join(
+            f"{n}: {buf[i + 1]} slots x {buf[i] / max(buf[i + 1], 1):.0f} cyc"
+            for i, n in ((10, "deg<=4"), (12, "deg 5-8"), (14, "deg>8"))))
     pre_ms = [e[0].elapsed_time(e[1]) for e in events]
     hub_ms = [e[1].elapsed_time(e[2]) for e in events]
     tile_ms = [e[2].elapsed_time(e[3]) for e in events]

@@ -1414,9 +1414,9 @@ __device__ __forceinline__ int opaque(int v) {
 }
 
 struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm queue)
-  int4 d;         // {row, e_begin, e_end, hub_rank}
-  int j;          // source of message (lane >> 3) of the first batch
-  bool live;      // slot < num_dst (otherwise d / j are a clamped copy, row taken as -1)
+  int v;          // lanes 0..3: {row, e_begin, e_end, hub_rank}; lanes 8..15: sources of
+                  // messages 0..7 (slot_cols); other lanes: row
+  bool live;      // slot < num_dst (otherwise v is a clamped copy, row taken as -1)
 };
 
 __device__ __forceinline__ int4 uni4(int4 v) {
@@ -1434,6 +1434,7 @@ struct SlotRows {  // first batch in flight
   static constexpr int PF = KF >= 3 ? 4 : 4;  // rows issued ahead (register budget)
   float th;        // t_i of head lane & 7
   float sj;        // s_j of the lane's message
+  int cj;          // source of message 8 + lane (0 past the end; nothing fetched for <= 8)
   float xv[PF][KF];  // x rows of messages 0..PF-1 (lane <-> feature)
 };
 
@@ -1441,9 +1442,9 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
                                        const int4* __restrict__ desc,
                                        const int32_t* __restrict__ cols8, int lane) {
   const int64_t sl = slot < num_dst ? slot : num_dst - 1;
-  const int z0 = opaque(0);  // divergent zero: a vector load, not s_load
-  p.d = desc[CHK(1, sl, 1) + z0];
-  p.j = cols8[CHK(2, sl, 1) * 8 + (lane >> 3)];
+  const int32_t* a = reinterpret_cast<const int32_t*>(desc + CHK(1, sl, 1)) + (lane & 3);
+  const int32_t* b = cols8 + CHK(2, sl, 1) * 8 + (lane & 7);
+  p.v = *((lane & 56) == 8 ? b : a);  // one dword per lane, one VGPR per slot
   p.live = slot < num_dst;
 }
 
@@ -1461,7 +1462,7 @@ __device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xr), 0, F * 4, 0x00020000);
 #pragma unroll
   for (int q = 0; q < KF; ++q)
-    v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (lane + 64 * q) * 4, 0, 0));
+    v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 256 * q, 0));
 }
 
 // Issue the first batch of a slot (PF rows, t_i, s_j) unconditionally (empty and
@@ -1470,19 +1471,31 @@ __device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int
 template <int KF>
 __device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF>& q,
                                          const float* __restrict__ x, int64_t ldx, int F,
+                                         const int32_t* __restrict__ col,
                                          const float* __restrict__ st, int64_t dst_offset,
                                          SlotRing* __restrict__ ring, int lane) {
   const int h = lane & 7;
-  const int row = __builtin_amdgcn_readfirstlane(p.d.x);  // >= 0: clamped slots are real rows
+  const int row = __builtin_amdgcn_readlane(p.v, 0);  // >= 0: clamped slots are real rows
+  const int e0 = __builtin_amdgcn_readlane(p.v, 1);
+  const int e1 = __builtin_amdgcn_readlane(p.v, 2);
+  const int hw = __builtin_amdgcn_readlane(p.v, 3);
+  const int jm = __builtin_amdgcn_ds_bpermute((8 + (lane >> 3)) << 2, p.v);  // source of message lane >> 3
   q.th = st[CHK(3, dst_offset + row, 0) * 16 + H + h];
-  q.sj = st[int64_t(CHK(4, p.j, 0)) * 16 + h];
+  q.sj = st[int64_t(CHK(4, jm, 0)) * 16 + h];
 #pragma unroll
   for (int k = 0; k < SlotRows<KF>::PF; ++k) {
-    const int jk = __builtin_amdgcn_readlane(p.j, 8 * k);
+    const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
     sl_rows<KF>(x + int64_t(CHK(5, jk, 0)) * ldx, F, lane, q.xv[k]);
   }
-  if (lane == 0) ring->d = make_int4(p.live ? p.d.x : -1, p.d.y, p.d.z, p.d.w);
-  if (h == 0) ring->j[lane >> 3] = p.j;
+  {  // sources of messages 8 .. 71 (one per lane), range-checked: light, hub and
+     // empty slots fetch nothing
+    const int nx = (p.live && hw < 0 && e1 - e0 > 8) ? e1 - e0 - 8 : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int32_t*>(col) + e0 + 8, 0, nx * 4, 0x00020000);
+    q.cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+  }
+  if (lane == 0) ring->d = make_int4(p.live ? row : -1, e0, e1, hw);
+  if ((lane & 56) == 8) ring->j[lane & 7] = p.v;
 }
 
 #ifdef GFD_SCALAR_AGG
@@ -1685,10 +1698,47 @@ __device__ __forceinline__ f32x2 bcast2(float v, int l0) {  // (v@l0, v@l0+1), w
                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l0 + 1))};
 }
 
+// x row of one message (wave-uniform source j) into lane <-> feature registers;
+// ok = false fetches nothing and reads zeros (range check on an empty buffer)
+template <int KF>
+__device__ __forceinline__ void sl_row(const float* __restrict__ x, int64_t ldx, int F, int lane,
+                                       int j, bool ok, float (&v)[KF]) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x) + int64_t(j) * ldx, 0, ok ? F * 4 : 0, 0x00020000);
+#pragma unroll
+  for (int q = 0; q < KF; ++q)
+    v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 256 * q, 0));
+}
+
+// z += p_k x_k for rows K0 .. K0 + kn - 1 of a batch (kn >= 1); the weights of
+// a message are broadcast as head pairs from lanes 8 k + 2 g (constant lanes)
+template <int KF, int K0>
+__device__ __forceinline__ void sl_fma4(f32x2 (&z)[4][KF], const float (&xr)[4][KF], float pv,
+                                        int kn) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k == 0 || k < kn) {
+      f32x2 p2[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * (K0 + k) + 2 * g);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int qq = 0; qq < KF; ++qq)
+          z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
+    }
+  }
+}
+
 // Un-normalised z of one slot, heads in pairs (z2[g] = heads 2g, 2g+1, lane <->
 // feature), and 1 / (sum + eps) of head lane & 7 (1 for hub rows, whose merged
-// z is already normalised).  Online softmax over batches of 8 messages, rows in
-// sub-batches of 4 (the first PF rows prefetched in q); packed FMAs.
+// z is already normalised).  Online softmax over batches of 8 messages.
+//  * batch 0: logits and rows 0..3 were issued one tile ahead (q); rows 4..7 are
+//    issued on entry.
+//  * batches 1..: sources come from the cj window (lane i = message cb + i,
+//    loaded at issue time), so the logits and all 8 rows of the next batch are
+//    issued together at the end of the current one (one memory round trip per
+//    batch; a col -> st -> rows chain would be three).
 template <int KF>
 __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const SlotRows<KF>& q,
                                             const float* __restrict__ x, int64_t ldx, int F,
@@ -1715,25 +1765,60 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
     return 1.0f;
   }
   const int e0 = CHK(12, d.y, 3), e1 = CHK(13, d.z, 3);
-  float m = -INFINITY, l = 0.f;
-  for (int b = e0; b < e1; b += 8) {
-    const int e = b + kk;
-    const bool valid = e < e1;
-    int j;
-    float v;
-    if (b == e0) {
-      j = j0;
-      v = leaky(q.sj + q.th, slope);
-    } else {
-      j = col[valid ? e : e1 - 1];
-      v = leaky(st[int64_t(CHK(7, j, 0)) * 16 + h] + q.th, slope);
+  const int n = e1 - e0;
+  float xa[4][KF], xb[4][KF];
+  const float keep = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+  // batch 0
+  float m, l;
+  {
+    const bool valid = kk < n;
+    const float v = leaky(q.sj + q.th, slope);
+    m = max_xor8_16_32(valid ? v : -INFINITY);
+    float pv = valid ? __expf(v - m) : 0.f;
+    l = pv;
+    if (dp > 0.f) pv = dropout_keep(seed, uint32_t(e0 + kk), uint32_t(h), dp) ? pv * keep : 0.f;
+    sl_fma4<KF, 0>(z, q.xv, pv, min(4, n));
+    if (n > 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        sl_row<KF>(x, ldx, F, lane, CHK(8, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), 0),
+                   4 + k < n, xb[k]);
+      sl_fma4<KF, 4>(z, xb, pv, min(4, n - 4));
     }
+  }
+  // batches 1..: loads of batch b issued at the end of batch b - 8
+  int cj = q.cj, cb = 8;  // cj window: lane i = message cb + i
+  float sv = 0.f;
+  auto issue = [&](int b) {
+    if (b - cb >= 64) {  // past the window (more than 72 messages): next 64 sources
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int32_t*>(col) + e0 + b, 0, (n - b) * 4, 0x00020000);
+      cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+      cb = b;
+    }
+    const int jl = __builtin_amdgcn_ds_bpermute((b - cb + kk) << 2, cj);
+    sv = st[int64_t(CHK(7, jl, 0)) * 16 + h];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      sl_row<KF>(x, ldx, F, lane, CHK(9, __builtin_amdgcn_readlane(cj, b - cb + k), 0),
+                 b + k < n, xa[k]);
+    if (n - b > 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        sl_row<KF>(x, ldx, F, lane, CHK(9, __builtin_amdgcn_readlane(cj, b - cb + 4 + k), 0),
+                   b + 4 + k < n, xb[k]);
+    }
+  };
+  if (n > 8) issue(8);
+  for (int b = 8; b < n; b += 8) {
+    const bool valid = b + kk < n;
+    const float v = leaky(sv + q.th, slope);
     const float bm = max_xor8_16_32(valid ? v : -INFINITY);
     const float mn = fmaxf(m, bm);
     const float sc = __expf(m - mn);
     float pv = valid ? __expf(v - mn) : 0.f;
     l = fmaf(l, sc, pv);
-    if (b != e0 && __any(sc != 1.0f)) {
+    if (__any(sc != 1.0f)) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x2 s2 = bcast2(sc, 2 * g);
@@ -1743,46 +1828,10 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
     }
     m = mn;
     if (dp > 0.f)
-      pv = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? pv * (1.0f / (1.0f - dp)) : 0.f;
-    const int nk = min(8, e1 - b);
-#pragma unroll
-    for (int k0 = 0; k0 < 8; k0 += 4) {  // unrolled: constant readlane lanes
-      if (k0 >= nk) break;
-      float xl[4][KF];
-      constexpr int PF = SlotRows<KF>::PF;
-      if (b == e0 && k0 == 0) {
-#pragma unroll
-        for (int k = 0; k < PF; ++k)
-#pragma unroll
-          for (int qq = 0; qq < KF; ++qq) xl[k][qq] = q.xv[k][qq];
-        if (PF < 4 && nk > PF) {
-#pragma unroll
-          for (int k = PF; k < 4; ++k) {
-            const int jk = __builtin_amdgcn_readlane(j, 8 * k);
-            sl_rows<KF>(x + int64_t(CHK(8, jk, 0)) * ldx, F, lane, xl[k]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int jk = __builtin_amdgcn_readlane(j, 8 * (k0 + k));
-          sl_rows<KF>(x + int64_t(CHK(9, jk, 0)) * ldx, F, lane, xl[k]);
-        }
-      }
-      const int kn = min(4, nk - k0);  // padding rows carry p = 0 anyway
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k == 0 || k < kn) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x2 p2 = bcast2(pv, 8 * (k0 + k) + 2 * g);
-#pragma unroll
-            for (int qq = 0; qq < KF; ++qq)
-              z[g][qq] = __builtin_elementwise_fma(p2, f32x2{xl[k][qq], xl[k][qq]}, z[g][qq]);
-          }
-        }
-      }
-    }
+      pv = dropout_keep(seed, uint32_t(e0 + b + kk), uint32_t(h), dp) ? pv * keep : 0.f;
+    sl_fma4<KF, 0>(z, xa, pv, min(4, n - b));
+    if (n - b > 4) sl_fma4<KF, 4>(z, xb, pv, min(4, n - b - 4));
+    if (b + 8 < n) issue(b + 8);
   }
   l = sum_xor8_16_32(l);
   if (stats && lane < 8) {
@@ -1806,6 +1855,9 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
                                          int* __restrict__ rid, int r, int lane PROF_PARAMS) {
   const int4 d = uni4(ring->d);
   const int j0 = ring->j[lane >> 3];
+#ifdef GFD_PROF
+  const uint64_t t_in = __builtin_readcyclecounter();
+#endif
   f32x2 z[4][KF];
   const float inv = sl_compute<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                                    stats, lane, z);
@@ -1847,6 +1899,15 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
     rsc[r] = ldexpf(1.0f, -er);
     rid[r] = d.x;
   }
+#ifdef GFD_PROF
+  // slot cycles by degree class: 10/11 deg <= 4, 12/13 5..8, 14/15 > 8 (hub rows skipped)
+  if (lane == 0 && d.x >= 0 && d.w < 0) {
+    const int deg = d.z - d.y;
+    const int c = deg <= 4 ? 10 : (deg <= 8 ? 12 : 14);
+    prof_lds[(threadIdx.x >> 6) * 16 + c] += __builtin_readcyclecounter() - t_in;
+    prof_lds[(threadIdx.x >> 6) * 16 + c + 1] += 1;
+  }
+#endif
 }
 
 #endif  // GFD_SCALAR_AGG
@@ -1928,8 +1989,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   // records of tile 2 loading
   sl_rec(n0, slot(0, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(0, r1), num_dst, desc, cols8, lane);
-  sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + r0, lane);
-  sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + r1, lane);
+  sl_issue<KF>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + r0, lane);
+  sl_issue<KF>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + r1, lane);
   sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
   if (nv > 0) {
@@ -1938,8 +1999,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     sl_store<KF>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
                  Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, lane PROF_PASS);
   }
-  sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + kTile + r0, lane);
-  sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + kTile + r1, lane);
+  sl_issue<KF>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + kTile + r0, lane);
+  sl_issue<KF>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + kTile + r1, lane);
   sl_rec(n0, slot(2, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(2, r1), num_dst, desc, cols8, lane);
   __syncthreads();
@@ -2022,8 +2083,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
                    stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r1,
                    lane PROF_PASS);
       PROF_MARK(4);
-      sl_issue<KF>(n0, d0, x, ldx, F, st, dst_offset, ring0 + par * kTile + r0, lane);
-      sl_issue<KF>(n1, d1, x, ldx, F, st, dst_offset, ring0 + par * kTile + r1, lane);
+      sl_issue<KF>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + par * kTile + r0, lane);
+      sl_issue<KF>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + par * kTile + r1, lane);
       sl_rec(n0, slot(v + 3, r0), num_dst, desc, cols8, lane);
       sl_rec(n1, slot(v + 3, r1), num_dst, desc, cols8, lane);
       PROF_MARK(5);
