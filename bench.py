@@ -222,10 +222,11 @@ def main():
     elapsed = time.perf_counter() - t0
     if os.environ.get("GFD_PROF_DUMP") and hasattr(lib, "gfd_debug_prof"):
         import ctypes
-        buf = (ctypes.c_ulonglong * 16)()
+        buf = (ctypes.c_ulonglong * 32)()
         lib.gfd_debug_prof(buf)
         names = {0: "mfma", 1: "barrier1", 2: "reduce", 8: "wait-rows", 9: "agg-compute",
-                 3: "agg-epilogue0", 4: "agg-epilogue1", 5: "issue", 6: "barrier2"}
+                 3: "agg-epilogue0", 4: "agg-epilogue1", 18: "drain", 16: "issue0", 17: "issue1",
+                 5: "records", 6: "barrier2"}
         tot = sum(buf[i] for i in names)
         log("[bench] k_stream phase cycles (summed over waves): " + ", ".join(
             f"{n} {buf[i] / max(tot, 1) * 100:.1f}%" for i, n in names.items()) +

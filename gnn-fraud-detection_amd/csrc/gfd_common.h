@@ -54,6 +54,8 @@ struct Sizer {
 };
 
 __device__ __forceinline__ float leaky(float v, float slope) { return v > 0.f ? v : v * slope; }
+// the same for 0 <= slope <= 1 (bit-identical, +-0 included): one multiply and one max
+__device__ __forceinline__ float leaky01(float v, float slope) { return fmaxf(v, v * slope); }
 
 // Round-to-nearest-even fp32 -> bf16 bits (inputs are finite here).
 __device__ __forceinline__ uint16_t bf16_bits(float f) {

@@ -1357,6 +1357,9 @@ __global__ void __launch_bounds__(1024, 4) k_pair(
 // ---------------------------------------------------------------------------
 // k_stream and its slot helpers (kernel comment below).
 constexpr int kSWaves = 8;
+#ifndef GFD_STREAM_AP  // A-fragment k-steps read ahead in the MFMA loop
+#define GFD_STREAM_AP 2
+#endif
 // k_stream phase ablation for diagnostic builds (-DGFD_STREAM_ABLATE=1: no MFMA,
 // 2: no aggregation); compile-time so the product kernel carries no branch
 #ifdef GFD_STREAM_ABLATE
@@ -1389,11 +1392,12 @@ __device__ __noinline__ void chk_fail(int site, long long v, long long lim) {
 // Phase cycle counters of k_stream (diagnostic builds only, -DGFD_PROF):
 // 0 MFMA, 1 barrier after MFMA, 2 reduce+store, 3 aggregate slot 0,
 // 4 aggregate slot 1, 5 issue+records, 6 barrier after aggregation, 7 tiles
-__device__ unsigned long long g_prof[16];
+constexpr int kProfN = 32;
+__device__ unsigned long long g_prof[kProfN];
 #define PROF_MARK(i)                                                              \
   do {                                                                            \
     const uint64_t t_ = __builtin_readcyclecounter();                             \
-    if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * 16 + (i)] += t_ - prof_t; \
+    if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * kProfN + (i)] += t_ - prof_t; \
     prof_t = t_;                                                                  \
   } while (0)
 #define PROF_PARAMS , uint64_t &prof_t, uint64_t *prof_lds
@@ -1429,9 +1433,9 @@ struct SlotRing {  // the same record parked in LDS between issue and aggregatio
   int j[8];
 };
 
-template <int KF>
+template <int KF, int PFN = 4>
 struct SlotRows {  // first batch in flight
-  static constexpr int PF = KF >= 3 ? 4 : 4;  // rows issued ahead (register budget)
+  static constexpr int PF = PFN;  // rows issued ahead (register budget)
   float th;        // t_i of head lane & 7
   float sj;        // s_j of the lane's message
   int cj;          // source of message 8 + lane (0 past the end; nothing fetched for <= 8)
@@ -1468,8 +1472,8 @@ __device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int
 // Issue the first batch of a slot (PF rows, t_i, s_j) unconditionally (empty and
 // hub slots read valid rows that are ignored, so no branch joins in-flight
 // loads) and park the record in the LDS ring for the aggregation.
-template <int KF>
-__device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF>& q,
+template <int KF, int PFN>
+__device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF, PFN>& q,
                                          const float* __restrict__ x, int64_t ldx, int F,
                                          const int32_t* __restrict__ col,
                                          const float* __restrict__ st, int64_t dst_offset,
@@ -1483,7 +1487,7 @@ __device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF>& q,
   q.th = st[CHK(3, dst_offset + row, 0) * 16 + H + h];
   q.sj = st[int64_t(CHK(4, jm, 0)) * 16 + h];
 #pragma unroll
-  for (int k = 0; k < SlotRows<KF>::PF; ++k) {
+  for (int k = 0; k < PFN; ++k) {
     const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
     sl_rows<KF>(x + int64_t(CHK(5, jk, 0)) * ldx, F, lane, q.xv[k]);
   }
@@ -1498,168 +1502,6 @@ __device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF>& q,
   if ((lane & 56) == 8) ring->j[lane & 7] = p.v;
 }
 
-#ifdef GFD_SCALAR_AGG
-// Normalised z of one slot (all 8 heads, lane <-> feature); online softmax over
-// batches of 8 messages, rows in sub-batches of 4; the first sub-batch is in q.
-template <int KF>
-__device__ __forceinline__ void sl_compute_s(const int4 d, const int j0, const SlotRows<KF>& q,
-                                           const float* __restrict__ x, int64_t ldx, int F,
-                                           int Fp, const int32_t* __restrict__ col,
-                                           const float* __restrict__ st, float slope, float dp,
-                                           uint64_t seed, const float* __restrict__ zhub,
-                                           float* __restrict__ stats, int lane,
-                                           float (&z)[H][KF]) {
-  const int h = lane & 7, kk = lane >> 3;
-#pragma unroll
-  for (int hh = 0; hh < H; ++hh)
-#pragma unroll
-    for (int qq = 0; qq < KF; ++qq) z[hh][qq] = 0.f;
-  if (d.x < 0) return;
-  if (d.w >= 0) {  // hub: merged row (already normalised)
-    const float* src = zhub + int64_t(d.w) * (H * Fp);
-#pragma unroll
-    for (int hh = 0; hh < H; ++hh)
-#pragma unroll
-      for (int qq = 0; qq < KF; ++qq) {
-        const int f = lane + 64 * qq;
-        z[hh][qq] = f < Fp ? src[hh * Fp + f] : 0.f;
-      }
-    return;
-  }
-  const int e0 = d.y, e1 = d.z;
-  float m = -INFINITY, l = 0.f;
-  for (int b = e0; b < e1; b += 8) {
-    const int e = b + kk;
-    const bool valid = e < e1;
-    int j;
-    float v;
-    if (b == e0) {
-      j = j0;
-      v = leaky(q.sj + q.th, slope);
-    } else {
-      j = col[valid ? e : e1 - 1];
-      v = leaky(st[int64_t(j) * 16 + h] + q.th, slope);
-    }
-    float bm = valid ? v : -INFINITY;
-    bm = fmaxf(bm, __shfl_xor(bm, 8));
-    bm = fmaxf(bm, __shfl_xor(bm, 16));
-    bm = fmaxf(bm, __shfl_xor(bm, 32));
-    const float mn = fmaxf(m, bm);
-    const float sc = __expf(m - mn);
-    float pv = valid ? __expf(v - mn) : 0.f;
-    l = fmaf(l, sc, pv);
-    if (b != e0 && __any(sc != 1.0f)) {
-#pragma unroll
-      for (int hh = 0; hh < H; ++hh) {
-        const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
-#pragma unroll
-        for (int qq = 0; qq < KF; ++qq) z[hh][qq] *= s;
-      }
-    }
-    m = mn;
-    if (dp > 0.f)
-      pv = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? pv * (1.0f / (1.0f - dp)) : 0.f;
-    const int nk = min(8, e1 - b);
-    for (int k0 = 0; k0 < nk; k0 += 4) {
-      float xl[4][KF];
-      constexpr int PF = SlotRows<KF>::PF;
-      if (b == e0 && k0 == 0) {
-#pragma unroll
-        for (int k = 0; k < PF; ++k)
-#pragma unroll
-          for (int qq = 0; qq < KF; ++qq) xl[k][qq] = q.xv[k][qq];
-        if (PF < 4 && nk > PF) {
-#pragma unroll
-          for (int k = PF; k < 4; ++k) {
-            const int jk = __builtin_amdgcn_readlane(j, 8 * k);
-            sl_rows<KF>(x + int64_t(jk) * ldx, F, lane, xl[k]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int jk = __builtin_amdgcn_readlane(j, 8 * (k0 + k));
-          sl_rows<KF>(x + int64_t(jk) * ldx, F, lane, xl[k]);
-        }
-      }
-      const int kn = min(4, nk - k0);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k == 0 || k < kn) {
-#pragma unroll
-          for (int hh = 0; hh < H; ++hh) {
-            const float pk =
-                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), 8 * (k0 + k) + hh));
-#pragma unroll
-            for (int qq = 0; qq < KF; ++qq) z[hh][qq] = fmaf(pk, xl[k][qq], z[hh][qq]);
-          }
-        }
-      }
-    }
-  }
-  l += __shfl_xor(l, 8);
-  l += __shfl_xor(l, 16);
-  l += __shfl_xor(l, 32);
-  if (stats && lane < 8) {
-    stats[int64_t(d.x) * 16 + lane] = m;
-    stats[int64_t(d.x) * 16 + 8 + lane] = l;
-  }
-  const float inv_lane = 1.0f / (l + kSoftmaxEps);
-#pragma unroll
-  for (int hh = 0; hh < H; ++hh) {
-    const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_lane), hh));
-#pragma unroll
-    for (int qq = 0; qq < KF; ++qq) z[hh][qq] *= inv;
-  }
-}
-
-template <int KF>
-__device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, const SlotRows<KF>& q,
-                                         const float* __restrict__ x, int64_t ldx, int F, int Fp,
-                                         const int32_t* __restrict__ col,
-                                         const float* __restrict__ st, float slope, float dp,
-                                         uint64_t seed, const float* __restrict__ zhub,
-                                         float* __restrict__ stats, _Float16* __restrict__ zh,
-                                         _Float16* __restrict__ zl, float* __restrict__ rsc,
-                                         int* __restrict__ rid, int r, int lane) {
-  const int4 d = uni4(ring->d);
-  const int j0 = ring->j[lane >> 3];
-  float z[H][KF];
-  sl_compute_s<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, lane, z);
-  float zm = 0.f;
-#pragma unroll
-  for (int hh = 0; hh < H; ++hh)
-#pragma unroll
-    for (int qq = 0; qq < KF; ++qq) zm = fmaxf(zm, fabsf(z[hh][qq]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) zm = fmaxf(zm, __shfl_xor(zm, o));
-  int ex = 0;
-  if (zm > 0.f) frexpf(zm, &ex);
-  int er = 14 - ex;
-  er = er > 100 ? 100 : (er < -100 ? -100 : er);
-  const float rs = ldexpf(1.0f, er);
-#pragma unroll
-  for (int qq = 0; qq < KF; ++qq) {
-    const int f = lane + 64 * qq;
-    if (f < Fp) {
-      union { f16x8 v; _Float16 h[8]; } a, b;
-#pragma unroll
-      for (int hh = 0; hh < H; ++hh) {
-        const float v = z[hh][qq] * rs;
-        const _Float16 hv = (_Float16)v;
-        a.h[hh] = hv;
-        b.h[hh] = (_Float16)(v - (float)hv);
-      }
-      *reinterpret_cast<f16x8*>(zh + 8 * f) = a.v;
-      *reinterpret_cast<f16x8*>(zl + 8 * f) = b.v;
-    }
-  }
-  if (lane == 0) {
-    rsc[r] = ldexpf(1.0f, -er);
-    rid[r] = d.x;
-  }
-}
-#else
 // In-register cross-lane reductions (DPP row rotate + gfx950 permlane swaps):
 // a few VALU cycles each instead of a ds_bpermute round trip through the LDS
 // unit per step (__shfl_xor).
@@ -1710,17 +1552,21 @@ __device__ __forceinline__ void sl_row(const float* __restrict__ x, int64_t ldx,
     v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 256 * q, 0));
 }
 
-// z += p_k x_k for rows K0 .. K0 + kn - 1 of a batch (kn >= 1); the weights of
-// a message are broadcast as head pairs from lanes 8 k + 2 g (constant lanes)
-template <int KF, int K0>
-__device__ __forceinline__ void sl_fma4(f32x2 (&z)[4][KF], const float (&xr)[4][KF], float pv,
-                                        int kn) {
+// z += p_k x_k for rows k0 .. k0 + kn - 1 of a batch (kn >= 1; k0 a constant
+// after unrolling); the weights of
+// a message are broadcast as head pairs from lanes 8 k + 2 g (constant lanes).
+// (Parking the weights in LDS and reading them back as two broadcast
+// ds_read_b128 per message saves the 8 v_readlane but exposes the LDS latency
+// in the FMA chain: measured slower with no VGPRs left to read ahead.)
+template <int KF, int NR>
+__device__ __forceinline__ void sl_fma(f32x2 (&z)[4][KF], const float (&xr)[NR][KF], float pv,
+                                       int k0, int kn) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < NR; ++k) {
     if (k == 0 || k < kn) {
       f32x2 p2[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * (K0 + k) + 2 * g);
+      for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * (k0 + k) + 2 * g);
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
@@ -1739,8 +1585,8 @@ __device__ __forceinline__ void sl_fma4(f32x2 (&z)[4][KF], const float (&xr)[4][
 //    loaded at issue time), so the logits and all 8 rows of the next batch are
 //    issued together at the end of the current one (one memory round trip per
 //    batch; a col -> st -> rows chain would be three).
-template <int KF>
-__device__ __forceinline__ float sl_compute(const int4 d, const int j0, const SlotRows<KF>& q,
+template <int KF, int PFN>
+__device__ __forceinline__ float sl_compute(const int4 d, const int j0, const SlotRows<KF, PFN>& q,
                                             const float* __restrict__ x, int64_t ldx, int F,
                                             int Fp, const int32_t* __restrict__ col,
                                             const float* __restrict__ st, float slope, float dp,
@@ -1772,18 +1618,22 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
   float m, l;
   {
     const bool valid = kk < n;
-    const float v = leaky(q.sj + q.th, slope);
+    const float v = leaky01(q.sj + q.th, slope);
     m = max_xor8_16_32(valid ? v : -INFINITY);
     float pv = valid ? __expf(v - m) : 0.f;
     l = pv;
     if (dp > 0.f) pv = dropout_keep(seed, uint32_t(e0 + kk), uint32_t(h), dp) ? pv * keep : 0.f;
-    sl_fma4<KF, 0>(z, q.xv, pv, min(4, n));
-    if (n > 4) {
+    sl_fma<KF, PFN>(z, q.xv, pv, 0, min(PFN, n));
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        sl_row<KF>(x, ldx, F, lane, CHK(8, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), 0),
-                   4 + k < n, xb[k]);
-      sl_fma4<KF, 4>(z, xb, pv, min(4, n - 4));
+    for (int k0 = PFN; k0 < 8; k0 += 4) {  // rest of the batch, 4 rows at a time
+      if (n > k0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          sl_row<KF>(x, ldx, F, lane,
+                     CHK(8, __builtin_amdgcn_readlane(j0, 8 * (k0 + k < 8 ? k0 + k : 7)), 0),
+                     k0 + k < n && k0 + k < 8, xb[k]);
+        sl_fma<KF, 4>(z, xb, pv, k0, min(4, min(n, 8) - k0));
+      }
     }
   }
   // batches 1..: loads of batch b issued at the end of batch b - 8
@@ -1812,7 +1662,7 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
   if (n > 8) issue(8);
   for (int b = 8; b < n; b += 8) {
     const bool valid = b + kk < n;
-    const float v = leaky(sv + q.th, slope);
+    const float v = leaky01(sv + q.th, slope);
     const float bm = max_xor8_16_32(valid ? v : -INFINITY);
     const float mn = fmaxf(m, bm);
     const float sc = __expf(m - mn);
@@ -1829,8 +1679,8 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
     m = mn;
     if (dp > 0.f)
       pv = dropout_keep(seed, uint32_t(e0 + b + kk), uint32_t(h), dp) ? pv * keep : 0.f;
-    sl_fma4<KF, 0>(z, xa, pv, min(4, n - b));
-    if (n - b > 4) sl_fma4<KF, 4>(z, xb, pv, min(4, n - b - 4));
+    sl_fma<KF, 4>(z, xa, pv, 0, min(4, n - b));
+    if (n - b > 4) sl_fma<KF, 4>(z, xb, pv, 4, min(4, n - b - 4));
     if (b + 8 < n) issue(b + 8);
   }
   l = sum_xor8_16_32(l);
@@ -1838,39 +1688,64 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
     stats[int64_t(CHK(11, d.x, 1)) * 16 + lane] = m;
     stats[int64_t(d.x) * 16 + 8 + lane] = l;
   }
-  return 1.0f / (l + kSoftmaxEps);
+  return __builtin_amdgcn_rcpf(l + kSoftmaxEps);
 }
 
-// Aggregate one slot (record from the LDS ring, first batch in q) and store its
-// Z row: normalised, power-of-two scaled (max |z| -> [2^13, 2^14)), feature-major
-// (K position 8 f + h), fp16 hi and unscaled lo', one 16-B store per feature each.
+// lo' = f16(t - f32(hi)) for both halves of a packed pair: one v_fma_mix each
+// (fp32 fma with an f16 operand, rounded to f16) instead of two conversions
+// back, a subtract and a pack
+__device__ __forceinline__ uint32_t split_lo(f32x2 t, uint32_t hi) {
+  uint32_t lo;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lo)
+      : "v"(t.x), "v"(t.y), "v"(hi));
+  return lo;
+}
+
+// One slot's Z row packed for the LDS tile: normalised, power-of-two scaled
+// (max |z| -> [2^13, 2^14)), feature-major (K position 8 f + h), fp16 hi and
+// unscaled lo' per feature (lane + 64 q).
 template <int KF>
-__device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, const SlotRows<KF>& q,
-                                         const float* __restrict__ x, int64_t ldx, int F, int Fp,
-                                         const int32_t* __restrict__ col,
-                                         const float* __restrict__ st, float slope, float dp,
-                                         uint64_t seed, const float* __restrict__ zhub,
-                                         float* __restrict__ stats, _Float16* __restrict__ zh,
-                                         _Float16* __restrict__ zl, float* __restrict__ rsc,
-                                         int* __restrict__ rid, int r, int lane PROF_PARAMS) {
+struct SlotZ {
+  f16x8 hi[KF], lo[KF];
+  int er;   // row scale exponent
+  int row;  // destination row (-1: empty slot)
+};
+
+// Aggregate one slot (record from the LDS ring, first batch in q) into registers.
+template <int KF, int PFN>
+__device__ __forceinline__ void sl_prep(const SlotRing* __restrict__ ring, const SlotRows<KF, PFN>& q,
+                                        const float* __restrict__ x, int64_t ldx, int F, int Fp,
+                                        const int32_t* __restrict__ col,
+                                        const float* __restrict__ st, float slope, float dp,
+                                        uint64_t seed, const float* __restrict__ zhub,
+                                        float* __restrict__ stats, SlotZ<KF>& o,
+                                        int lane PROF_PARAMS) {
   const int4 d = uni4(ring->d);
   const int j0 = ring->j[lane >> 3];
 #ifdef GFD_PROF
   const uint64_t t_in = __builtin_readcyclecounter();
 #endif
   f32x2 z[4][KF];
-  const float inv = sl_compute<KF>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+  const float inv = sl_compute<KF, PFN>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                                    stats, lane, z);
   PROF_MARK(9);
+  // row scale from max |z_h| * inv_h (rounding is monotonic, so this equals the
+  // max of the normalised values); normalisation and scale in one multiplier
+  // per head pair (inv * 2^er is exact)
+  f32x2 i2[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) i2[g] = bcast2(inv, 2 * g);
   float zm = 0.f;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const f32x2 i2 = bcast2(inv, 2 * g);
+    f32x2 a = {fabsf(z[g][0].x), fabsf(z[g][0].y)};
 #pragma unroll
-    for (int qq = 0; qq < KF; ++qq) {
-      z[g][qq] *= i2;
-      zm = fmaxf(zm, fmaxf(fabsf(z[g][qq].x), fabsf(z[g][qq].y)));
-    }
+    for (int qq = 1; qq < KF; ++qq)
+      a = f32x2{fmaxf(a.x, fabsf(z[g][qq].x)), fmaxf(a.y, fabsf(z[g][qq].y))};
+    a *= i2[g];
+    zm = fmaxf(zm, fmaxf(a.x, a.y));
   }
   zm = max_wave(zm);
   int ex = 0;
@@ -1878,39 +1753,67 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
   int er = 14 - ex;
   er = er > 100 ? 100 : (er < -100 ? -100 : er);
   const float rs = ldexpf(1.0f, er);
-  const f32x2 rs2 = {rs, rs};
+  f32x2 s2[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) s2[g] = i2[g] * f32x2{rs, rs};
 #pragma unroll
   for (int qq = 0; qq < KF; ++qq) {
-    const int f = lane + 64 * qq;
-    if (f < Fp) {
-      union { f16x8 v; f16x2 p[4]; } a, b;
+    union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } a, b;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {  // per head pair: cvt_pk, 2 cvt back, pk_add, cvt_pk
-        const f32x2 v = z[g][qq] * rs2;
-        const f16x2 hv = __builtin_convertvector(v, f16x2);
-        a.p[g] = hv;
-        b.p[g] = __builtin_convertvector(v - __builtin_convertvector(hv, f32x2), f16x2);
-      }
-      *reinterpret_cast<f16x8*>(zh + 8 * f) = a.v;
-      *reinterpret_cast<f16x8*>(zl + 8 * f) = b.v;
+    for (int g = 0; g < 4; ++g) {  // per head pair: pk_mul, cvt_pk, 2 fma_mix
+      const f32x2 t = z[g][qq] * s2[g];
+      a.p[g] = __builtin_convertvector(t, f16x2);
+      b.u[g] = split_lo(t, a.u[g]);
     }
+    o.hi[qq] = a.v;
+    o.lo[qq] = b.v;
   }
-  if (lane == 0) {
-    rsc[r] = ldexpf(1.0f, -er);
-    rid[r] = d.x;
-  }
+  o.er = er;
+  o.row = d.x;
 #ifdef GFD_PROF
   // slot cycles by degree class: 10/11 deg <= 4, 12/13 5..8, 14/15 > 8 (hub rows skipped)
   if (lane == 0 && d.x >= 0 && d.w < 0) {
     const int deg = d.z - d.y;
     const int c = deg <= 4 ? 10 : (deg <= 8 ? 12 : 14);
-    prof_lds[(threadIdx.x >> 6) * 16 + c] += __builtin_readcyclecounter() - t_in;
-    prof_lds[(threadIdx.x >> 6) * 16 + c + 1] += 1;
+    prof_lds[(threadIdx.x >> 6) * kProfN + c] += __builtin_readcyclecounter() - t_in;
+    prof_lds[(threadIdx.x >> 6) * kProfN + c + 1] += 1;
   }
 #endif
 }
 
-#endif  // GFD_SCALAR_AGG
+// Store a prepared row into the Z tile (one 16-B write per feature and plane).
+template <int KF>
+__device__ __forceinline__ void sl_write(const SlotZ<KF>& o, int Fp, _Float16* __restrict__ zh,
+                                         _Float16* __restrict__ zl, float* __restrict__ rsc,
+                                         int* __restrict__ rid, int r, int lane) {
+#pragma unroll
+  for (int qq = 0; qq < KF; ++qq) {
+    const int f = lane + 64 * qq;
+    if (f < Fp) {
+      *reinterpret_cast<f16x8*>(zh + 8 * f) = o.hi[qq];
+      *reinterpret_cast<f16x8*>(zl + 8 * f) = o.lo[qq];
+    }
+  }
+  if (lane == 0) {
+    rsc[r] = ldexpf(1.0f, -o.er);
+    rid[r] = o.row;
+  }
+}
+
+template <int KF, int PFN>
+__device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, const SlotRows<KF, PFN>& q,
+                                         const float* __restrict__ x, int64_t ldx, int F, int Fp,
+                                         const int32_t* __restrict__ col,
+                                         const float* __restrict__ st, float slope, float dp,
+                                         uint64_t seed, const float* __restrict__ zhub,
+                                         float* __restrict__ stats, _Float16* __restrict__ zh,
+                                         _Float16* __restrict__ zl, float* __restrict__ rsc,
+                                         int* __restrict__ rid, int r, int lane PROF_PARAMS) {
+  SlotZ<KF> o;
+  sl_prep<KF, PFN>(ring, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, o, lane PROF_PASS);
+  sl_write<KF>(o, Fp, zh, zl, rsc, rid, r, lane);
+}
+
 
 // Weight-stationary streaming tile kernel (persistent, one 8-wave block per CU,
 // two waves per SIMD at up to 256 VGPRs).
@@ -1979,30 +1882,25 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   }
 
 #ifdef GFD_PROF
-  __shared__ uint64_t prof_lds[kSWaves * 16];
-  if (lane < 16) prof_lds[wave * 16 + lane] = 0;
+  __shared__ uint64_t prof_lds[kSWaves * kProfN];
+  if (lane < kProfN) prof_lds[wave * kProfN + lane] = 0;
   uint64_t prof_t = __builtin_readcyclecounter();
 #endif
   SlotRec n0, n1;
   SlotRows<KF> d0, d1;
-  // prologue: rows of tile 0 issued, its Z aggregated; rows of tile 1 in flight;
-  // records of tile 2 loading
+  // prologue: tile 0 issued and aggregated; records of tile 1 loading
   sl_rec(n0, slot(0, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(0, r1), num_dst, desc, cols8, lane);
-  sl_issue<KF>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + r0, lane);
-  sl_issue<KF>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + r1, lane);
+  sl_issue<KF, 4>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + r0, lane);
+  sl_issue<KF, 4>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + r1, lane);
   sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
   if (nv > 0) {
-    sl_store<KF>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+    sl_store<KF, 4>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
                  Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, lane PROF_PASS);
-    sl_store<KF>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+    sl_store<KF, 4>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
                  Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, lane PROF_PASS);
   }
-  sl_issue<KF>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + kTile + r0, lane);
-  sl_issue<KF>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + kTile + r1, lane);
-  sl_rec(n0, slot(2, r0), num_dst, desc, cols8, lane);
-  sl_rec(n1, slot(2, r1), num_dst, desc, cols8, lane);
   __syncthreads();
 
   for (int64_t v = 0; v < nv; ++v) {
@@ -2016,7 +1914,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     // A fragments (and LDS-resident W_lo) AP k-steps ahead; the scheduling
     // barriers keep the compiler from hoisting every LDS read of the tile
     // (registers belong to W)
-    constexpr int AP = 2;
+    constexpr int AP = GFD_STREAM_AP;
     f16x8 phi[AP], plo[AP], pwl[AP];
 #pragma unroll
     for (int u = 0; u < AP; ++u) {
@@ -2027,8 +1925,23 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
         pwl[u] = *reinterpret_cast<const f16x8*>(&w);
       }
     }
+    const int pn = par ^ 1;
+    const bool more = v + 1 < nv;
 #pragma unroll
     for (int u = 0; u < KHM; ++u) {
+      // the next tile's first rows are issued between the k-steps: the vector
+      // memory pipe is idle in this phase (issued all at once after the
+      // aggregation, the 16 slots' loads queued behind each other).  Issued
+      // unconditionally (past the last tile: clamped, ignored records), so no
+      // copy of the previous rows has to stay live through the MFMA loop
+      if (u == 0) {
+        sl_issue<KF, 4>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + pn * kTile + r0, lane);
+        sl_rec(n0, slot(v + 2, r0), num_dst, desc, cols8, lane);
+      }
+      if (u == KHM / 2) {
+        sl_issue<KF, 4>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + pn * kTile + r1, lane);
+        sl_rec(n1, slot(v + 2, r1), num_dst, desc, cols8, lane);
+      }
       if (u < KH && kAblate != 1) {
         const f16x8 ahi = phi[u % AP], alo = plo[u % AP];
         f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % AP];
@@ -2067,36 +1980,30 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       }
     }
 
-    // ---- tile v + 1: aggregate its rows into Z; issue tile v + 2, load v + 3 ----
+    // ---- tile v + 1: aggregate its rows into Z ----
     PROF_MARK(2);
-    if (v + 1 < nv && kAblate != 2) {
-      const int pn = par ^ 1;
+    if (more && kAblate != 2) {
 #ifdef GFD_PROF_WAIT  // diagnostic: time the wait for the prefetched rows separately
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       PROF_MARK(8);
 #endif
-      sl_store<KF>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
-                   stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r0,
-                   lane PROF_PASS);
+      sl_store<KF, 4>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+                   stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile,
+                   r0, lane PROF_PASS);
       PROF_MARK(3);
-      sl_store<KF>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
-                   stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile, r1,
-                   lane PROF_PASS);
+      sl_store<KF, 4>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+                   stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile,
+                   r1, lane PROF_PASS);
       PROF_MARK(4);
-      sl_issue<KF>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + par * kTile + r0, lane);
-      sl_issue<KF>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + par * kTile + r1, lane);
-      sl_rec(n0, slot(v + 3, r0), num_dst, desc, cols8, lane);
-      sl_rec(n1, slot(v + 3, r1), num_dst, desc, cols8, lane);
-      PROF_MARK(5);
     }
     __syncthreads();  // Z of the next tile complete; reduce reads done
     PROF_MARK(6);
 #ifdef GFD_PROF
-    if (lane == 0) prof_lds[wave * 16 + 7] += 1;
+    if (lane == 0) prof_lds[wave * kProfN + 7] += 1;
 #endif
   }
 #ifdef GFD_PROF
-  if (lane < 16) atomicAdd(&g_prof[lane], (unsigned long long)prof_lds[wave * 16 + lane]);
+  if (lane < kProfN) atomicAdd(&g_prof[lane], (unsigned long long)prof_lds[wave * kProfN + lane]);
 #endif
 }
 
@@ -2346,6 +2253,7 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
   const size_t lds = stream_smem(L.Fp, LO);
   if (L.KS / 2 > KHM || lds > kLdsBytes || !a.plan.slot_cols) return GFD_ERR_UNSUPPORTED;
+  if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
   static size_t attr_lds = 0;  // dynamic LDS the attribute currently allows
   if (lds > attr_lds) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -2519,11 +2427,11 @@ int gfd_debug_chk(long long* host4) {
 
 #ifdef GFD_PROF
 // diagnostic builds: k_stream phase cycles summed over waves (see g_prof); reset after read
-int gfd_debug_prof(unsigned long long* host16) {
+int gfd_debug_prof(unsigned long long* host32) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) != hipSuccess)
+  if (hipMemcpyFromSymbol(host32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * kProfN) != hipSuccess)
     return -1;
-  unsigned long long z[16] = {};
+  unsigned long long z[kProfN] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

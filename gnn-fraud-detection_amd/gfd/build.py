@@ -27,11 +27,12 @@ LIB = os.path.join(PKG, f"libgfd_{VARIANT}.so" if VARIANT else "libgfd.so")
 OBJDIR = os.path.join(ROOT, "build", f"obj_{VARIANT}" if VARIANT else "obj")
 ARCH = os.environ.get("GFD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+# -fno-honor-nans: fmaxf without operand canonicalisation, so the DPP row
+# rotations fold into v_max_f32_dpp (no kernel relies on NaN semantics)
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+         "-fno-honor-nans",
          f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
-if VARIANT == "scalar":
-    FLAGS.append("-DGFD_SCALAR_AGG")
-elif VARIANT == "prof":
+if VARIANT == "prof":
     FLAGS.append("-DGFD_PROF")
 elif VARIANT == "profw":  # prof + a separate wait for the prefetched rows
     FLAGS += ["-DGFD_PROF", "-DGFD_PROF_WAIT"]
