@@ -1397,10 +1397,10 @@ __device__ unsigned long long g_prof[kProfN];
 #define PROF_MARK(i)                                                              \
   do {                                                                            \
     const uint64_t t_ = __builtin_readcyclecounter();                             \
-    if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * kProfN + (i)] += t_ - prof_t; \
+    if ((threadIdx.x & 63) == 0) prof_lds[(threadIdx.x >> 6) * kProfN + (i)] += uint32_t(t_ - prof_t); \
     prof_t = t_;                                                                  \
   } while (0)
-#define PROF_PARAMS , uint64_t &prof_t, uint64_t *prof_lds
+#define PROF_PARAMS , uint64_t &prof_t, uint32_t *prof_lds
 #define PROF_PASS , prof_t, prof_lds
 #else
 #define PROF_MARK(i)
@@ -1775,7 +1775,7 @@ __device__ __forceinline__ void sl_prep(const SlotRing* __restrict__ ring, const
   if (lane == 0 && d.x >= 0 && d.w < 0) {
     const int deg = d.z - d.y;
     const int c = deg <= 4 ? 10 : (deg <= 8 ? 12 : 14);
-    prof_lds[(threadIdx.x >> 6) * kProfN + c] += __builtin_readcyclecounter() - t_in;
+    prof_lds[(threadIdx.x >> 6) * kProfN + c] += uint32_t(__builtin_readcyclecounter() - t_in);
     prof_lds[(threadIdx.x >> 6) * kProfN + c + 1] += 1;
   }
 #endif
@@ -1846,8 +1846,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
   _Float16* Zh = reinterpret_cast<_Float16*>(ssm);              // [16][ZS]
   _Float16* Zl = Zh + kTile * ZS;                               // [16][ZS]
-  f32x4* red = reinterpret_cast<f32x4*>(Zl + kTile * ZS);       // [4 ct][64]
-  SlotRing* ring0 = reinterpret_cast<SlotRing*>(red + 4 * 64);  // [2 parity][16]
+  f32x4* red0 = reinterpret_cast<f32x4*>(Zl + kTile * ZS);      // [2 parity][4 ct][64]
+  SlotRing* ring0 = reinterpret_cast<SlotRing*>(red0 + 2 * 4 * 64);  // [2 parity][16]
   float* rsc0 = reinterpret_cast<float*>(ring0 + 2 * kTile);    // [2][16] by tile parity
   int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);         // [2][16]
   uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);       // [8 waves][LO][64]
@@ -1882,7 +1882,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   }
 
 #ifdef GFD_PROF
-  __shared__ uint64_t prof_lds[kSWaves * kProfN];
+  __shared__ uint32_t prof_lds[kSWaves * kProfN];
   if (lane < kProfN) prof_lds[wave * kProfN + lane] = 0;
   uint64_t prof_t = __builtin_readcyclecounter();
 #endif
@@ -1903,6 +1903,21 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   }
   __syncthreads();
 
+  // out rows of a finished tile (waves kh = 0): own K-half partial + the other
+  // half's from LDS, row scale, bias
+  auto reduce_store = [&](const f32x4& acc, int tpar) {
+    const float* rsc = rsc0 + tpar * kTile;
+    const int* rid = rid0 + tpar * kTile;
+    const f32x4 sum = acc + red0[(tpar * 4 + ct) * 64 + lane];
+    const int n = ct * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (lane >> 4) * 4 + q;
+      const int ri = rid[r];
+      if (ri >= 0) out[int64_t(CHK(10, ri, 1)) * C + n] = sum[q] * (rsc[r] * wu) + bcol;
+    }
+  };
+  f32x4 acc_prev = {0.f, 0.f, 0.f, 0.f};  // kh = 0: tile v - 1, stored during MFMA(v)
   for (int64_t v = 0; v < nv; ++v) {
     lane = opaque(threadIdx.x & 63);
     const int par = int(v & 1);
@@ -1942,6 +1957,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
         sl_issue<KF, 4>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + pn * kTile + r1, lane);
         sl_rec(n1, slot(v + 2, r1), num_dst, desc, cols8, lane);
       }
+      if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
       if (u < KH && kAblate != 1) {
         const f16x8 ahi = phi[u % AP], alo = plo[u % AP];
         f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % AP];
@@ -1961,24 +1977,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       }
     }
     acc0 += acc1;
-    if (kh) red[ct * 64 + lane] = acc0;
+    if (kh) red0[(par * 4 + ct) * 64 + lane] = acc0;
+    acc_prev = acc0;
     PROF_MARK(0);
     __syncthreads();  // partials visible; every Z read of this tile done
     PROF_MARK(1);
-
-    // ---- reduce + store: waves 0-3, column tile ct ----
-    if (!kh) {
-      const float* rsc = rsc0 + par * kTile;
-      const int* rid = rid0 + par * kTile;
-      const f32x4 sum = acc0 + red[ct * 64 + lane];
-      const int n = ct * 16 + (lane & 15);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = (lane >> 4) * 4 + q;
-        const int ri = rid[r];
-        if (ri >= 0) out[int64_t(CHK(10, ri, 1)) * C + n] = sum[q] * (rsc[r] * wu) + bcol;
-      }
-    }
 
     // ---- tile v + 1: aggregate its rows into Z ----
     PROF_MARK(2);
@@ -1996,19 +1999,20 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
                    r1, lane PROF_PASS);
       PROF_MARK(4);
     }
-    __syncthreads();  // Z of the next tile complete; reduce reads done
+    __syncthreads();  // Z of the next tile complete
     PROF_MARK(6);
 #ifdef GFD_PROF
     if (lane == 0) prof_lds[wave * kProfN + 7] += 1;
 #endif
   }
+  if (nv > 0 && !kh) reduce_store(acc_prev, int((nv - 1) & 1));  // last tile
 #ifdef GFD_PROF
   if (lane < kProfN) atomicAdd(&g_prof[lane], (unsigned long long)prof_lds[wave * kProfN + lane]);
 #endif
 }
 
 size_t stream_smem(int Fp, int lo) {
-  return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 4 * 64 +
+  return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 2 * 4 * 64 +
          sizeof(SlotRing) * 2 * kTile + sizeof(float) * 4 * kTile +
          sizeof(uint4) * kSWaves * lo * 64;
 }
