@@ -1472,34 +1472,50 @@ __device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int
 // Issue the first batch of a slot (PF rows, t_i, s_j) unconditionally (empty and
 // hub slots read valid rows that are ignored, so no branch joins in-flight
 // loads) and park the record in the LDS ring for the aggregation.
+// One piece of the issue of a slot's first batch: part 0 = logits (t_i, s_j),
+// the source window and the ring record; part 1 + k = x row k.  The stream
+// kernel spreads the parts over the MFMA k-steps.
+template <int PART, int KF, int PFN>
+__device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, PFN>& q,
+                                              const float* __restrict__ x, int64_t ldx, int F,
+                                              const int32_t* __restrict__ col,
+                                              const float* __restrict__ st, int64_t dst_offset,
+                                              SlotRing* __restrict__ ring, int lane) {
+  if constexpr (PART == 0) {
+    const int h = lane & 7;
+    const int row = __builtin_amdgcn_readlane(p.v, 0);  // >= 0: clamped slots are real rows
+    const int e0 = __builtin_amdgcn_readlane(p.v, 1);
+    const int e1 = __builtin_amdgcn_readlane(p.v, 2);
+    const int hw = __builtin_amdgcn_readlane(p.v, 3);
+    const int jm = __builtin_amdgcn_ds_bpermute((8 + (lane >> 3)) << 2, p.v);  // message lane >> 3
+    q.th = st[CHK(3, dst_offset + row, 0) * 16 + H + h];
+    q.sj = st[int64_t(CHK(4, jm, 0)) * 16 + h];
+    // sources of messages 8 .. 71 (one per lane), range-checked: light, hub and
+    // empty slots fetch nothing
+    const int nx = (p.live && hw < 0 && e1 - e0 > 8) ? e1 - e0 - 8 : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int32_t*>(col) + e0 + 8, 0, nx * 4, 0x00020000);
+    q.cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+    if (lane == 0) ring->d = make_int4(p.live ? row : -1, e0, e1, hw);
+    if ((lane & 56) == 8) ring->j[lane & 7] = p.v;
+  } else {
+    constexpr int k = PART - 1;
+    const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
+    sl_rows<KF>(x + int64_t(CHK(5, jk, 0)) * ldx, F, lane, q.xv[k]);
+  }
+}
+
 template <int KF, int PFN>
 __device__ __forceinline__ void sl_issue(const SlotRec& p, SlotRows<KF, PFN>& q,
                                          const float* __restrict__ x, int64_t ldx, int F,
                                          const int32_t* __restrict__ col,
                                          const float* __restrict__ st, int64_t dst_offset,
                                          SlotRing* __restrict__ ring, int lane) {
-  const int h = lane & 7;
-  const int row = __builtin_amdgcn_readlane(p.v, 0);  // >= 0: clamped slots are real rows
-  const int e0 = __builtin_amdgcn_readlane(p.v, 1);
-  const int e1 = __builtin_amdgcn_readlane(p.v, 2);
-  const int hw = __builtin_amdgcn_readlane(p.v, 3);
-  const int jm = __builtin_amdgcn_ds_bpermute((8 + (lane >> 3)) << 2, p.v);  // source of message lane >> 3
-  q.th = st[CHK(3, dst_offset + row, 0) * 16 + H + h];
-  q.sj = st[int64_t(CHK(4, jm, 0)) * 16 + h];
-#pragma unroll
-  for (int k = 0; k < PFN; ++k) {
-    const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
-    sl_rows<KF>(x + int64_t(CHK(5, jk, 0)) * ldx, F, lane, q.xv[k]);
-  }
-  {  // sources of messages 8 .. 71 (one per lane), range-checked: light, hub and
-     // empty slots fetch nothing
-    const int nx = (p.live && hw < 0 && e1 - e0 > 8) ? e1 - e0 - 8 : 0;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<int32_t*>(col) + e0 + 8, 0, nx * 4, 0x00020000);
-    q.cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
-  }
-  if (lane == 0) ring->d = make_int4(p.live ? row : -1, e0, e1, hw);
-  if ((lane & 56) == 8) ring->j[lane & 7] = p.v;
+  sl_issue_part<0>(p, q, x, ldx, F, col, st, dst_offset, ring, lane);
+  sl_issue_part<1>(p, q, x, ldx, F, col, st, dst_offset, ring, lane);
+  if constexpr (PFN > 1) sl_issue_part<2>(p, q, x, ldx, F, col, st, dst_offset, ring, lane);
+  if constexpr (PFN > 2) sl_issue_part<3>(p, q, x, ldx, F, col, st, dst_offset, ring, lane);
+  if constexpr (PFN > 3) sl_issue_part<4>(p, q, x, ldx, F, col, st, dst_offset, ring, lane);
 }
 
 // In-register cross-lane reductions (DPP row rotate + gfx950 permlane swaps):
@@ -1949,14 +1965,27 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       // aggregation, the 16 slots' loads queued behind each other).  Issued
       // unconditionally (past the last tile: clamped, ignored records), so no
       // copy of the previous rows has to stay live through the MFMA loop
-      if (u == 0) {
-        sl_issue<KF, 4>(n0, d0, x, ldx, F, col, st, dst_offset, ring0 + pn * kTile + r0, lane);
+      // the 10 issue pieces (per slot: header, 4 rows) spread evenly over the
+      // k-steps: piece i in k-step i * KHM / 10
+      SlotRing* rg = ring0 + pn * kTile;
+#define GFD_PIECE(i) (u == (i) * KHM / 10)
+      if (GFD_PIECE(0)) sl_issue_part<0>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(1)) sl_issue_part<1>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(2)) sl_issue_part<2>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(3)) sl_issue_part<3>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(4)) {
+        sl_issue_part<4>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
         sl_rec(n0, slot(v + 2, r0), num_dst, desc, cols8, lane);
       }
-      if (u == KHM / 2) {
-        sl_issue<KF, 4>(n1, d1, x, ldx, F, col, st, dst_offset, ring0 + pn * kTile + r1, lane);
+      if (GFD_PIECE(5)) sl_issue_part<0>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(6)) sl_issue_part<1>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(7)) sl_issue_part<2>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(8)) sl_issue_part<3>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(9)) {
+        sl_issue_part<4>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
         sl_rec(n1, slot(v + 2, r1), num_dst, desc, cols8, lane);
       }
+#undef GFD_PIECE
       if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
       if (u < KH && kAblate != 1) {
         const f16x8 ahi = phi[u % AP], alo = plo[u % AP];
