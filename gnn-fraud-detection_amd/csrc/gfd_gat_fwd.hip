@@ -65,18 +65,33 @@ struct PackHeader {  // device-side, written by k_wmax
 };
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_wmax(const float* __restrict__ W, int n,
-                                              PackHeader* __restrict__ hdr) {
-  __shared__ float red[256];
-  float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(W[i]));
-  red[threadIdx.x] = m;
+__global__ void __launch_bounds__(1024) k_wmax(const float* __restrict__ W, int n,
+                                               PackHeader* __restrict__ hdr) {
+  // one block; 16-B loads when W is aligned, four independent chains per thread
+  __shared__ float red[1024];
+  const int t = threadIdx.x;
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+  int i0 = 0;
+  if ((reinterpret_cast<uintptr_t>(W) & 15) == 0) {
+    const f32x4* W4 = reinterpret_cast<const f32x4*>(W);
+    const int n4 = n >> 2;
+    for (int i = t; i < n4; i += 1024) {
+      const f32x4 w = W4[i];
+      m0 = fmaxf(m0, fabsf(w.x));
+      m1 = fmaxf(m1, fabsf(w.y));
+      m2 = fmaxf(m2, fabsf(w.z));
+      m3 = fmaxf(m3, fabsf(w.w));
+    }
+    i0 = n4 << 2;
+  }
+  for (int i = i0 + t; i < n; i += 1024) m0 = fmaxf(m0, fabsf(W[i]));
+  red[t] = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+  for (int s = 512; s > 0; s >>= 1) {
+    if (t < s) red[t] = fmaxf(red[t], red[t + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     const float wm = red[0] * (1.0f / H);  // the packed values are W / H
     int ex = 0;
     if (wm > 0.f) frexpf(wm, &ex);         // wm < 2^ex
@@ -2077,78 +2092,71 @@ __global__ void __launch_bounds__(256) k_hub_partial(
 
 // Per hub: M_h = max_c m_ch, S_h = sum_c S_ch e^(m_ch - M_h).  One wave per hub,
 // lanes over chunks.  Writes hubstat[hub][16] and the backward stats.
-__global__ void __launch_bounds__(256) k_hub_stats(const float* __restrict__ part, int Fp,
-                                                   const int32_t* __restrict__ chunk_ptr,
-                                                   const int32_t* __restrict__ hub_dst,
-                                                   int64_t num_hubs, float* __restrict__ hubstat,
-                                                   float* __restrict__ stats) {
+// Hub finalisation, one wave per (hub, K slice of 256 values): global (max,
+// sum) per head over the hub's chunk partials (lanes over chunks), then the
+// slice of the merged, normalised z row (16-B loads, chunks unrolled by 4).
+// Fp is a multiple of 8, so a 4-wide group never straddles heads.
+__global__ void __launch_bounds__(256) k_hub_fin(const float* __restrict__ part, int Fp,
+                                                 const int32_t* __restrict__ chunk_ptr,
+                                                 const int32_t* __restrict__ hub_dst,
+                                                 int64_t num_hubs, int slices,
+                                                 float* __restrict__ stats,
+                                                 float* __restrict__ zhub) {
   const int lane = threadIdx.x & 63;
-  const int64_t hb = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  const int64_t wid = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  const int64_t hb = wid / slices;
+  const int sl = int(wid - hb * slices);
   if (hb >= num_hubs) return;
-  const int64_t stride = 16 + int64_t(H) * Fp;
+  const int KP = H * Fp;
+  const int64_t stride = 16 + KP;
   const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
   float M[H], S[H];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) { M[hh] = -INFINITY; S[hh] = 0.f; }
-  for (int c = c0 + lane; c < c1; c += 64)
-#pragma unroll
-    for (int hh = 0; hh < H; ++hh) M[hh] = fmaxf(M[hh], part[c * stride + hh]);
+  for (int c = c0 + lane; c < c1; c += 64) {
+    const f32x4* pr = reinterpret_cast<const f32x4*>(part + c * stride);
+    const f32x4 a = pr[0], b = pr[1];
+    M[0] = fmaxf(M[0], a.x); M[1] = fmaxf(M[1], a.y); M[2] = fmaxf(M[2], a.z); M[3] = fmaxf(M[3], a.w);
+    M[4] = fmaxf(M[4], b.x); M[5] = fmaxf(M[5], b.y); M[6] = fmaxf(M[6], b.z); M[7] = fmaxf(M[7], b.w);
+  }
 #pragma unroll
   for (int hh = 0; hh < H; ++hh)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) M[hh] = fmaxf(M[hh], __shfl_xor(M[hh], o));
-  for (int c = c0 + lane; c < c1; c += 64)
+  for (int c = c0 + lane; c < c1; c += 64) {
+    const float* pr = part + c * stride;
 #pragma unroll
-    for (int hh = 0; hh < H; ++hh) S[hh] += part[c * stride + 8 + hh] * __expf(part[c * stride + hh] - M[hh]);
+    for (int hh = 0; hh < H; ++hh) S[hh] += pr[8 + hh] * __expf(pr[hh] - M[hh]);
+  }
 #pragma unroll
   for (int hh = 0; hh < H; ++hh)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) S[hh] += __shfl_xor(S[hh], o);
-  if (lane == 0) {
+  if (stats && sl == 0 && lane < H) {
     const int64_t i = hub_dst[hb];
+    float m = M[0], ssum = S[0];
 #pragma unroll
-    for (int hh = 0; hh < H; ++hh) {
-      hubstat[hb * 16 + hh] = M[hh];
-      hubstat[hb * 16 + 8 + hh] = S[hh];
-      if (stats) {
-        stats[i * 16 + hh] = M[hh];
-        stats[i * 16 + 8 + hh] = S[hh];
-      }
-    }
+    for (int hh = 1; hh < H; ++hh)
+      if (lane == hh) { m = M[hh]; ssum = S[hh]; }
+    stats[i * 16 + lane] = m;
+    stats[i * 16 + 8 + lane] = ssum;
   }
+  const int k4 = sl * 64 + lane;
+  if (k4 >= KP / 4) return;
+  const int hh = (4 * k4) / Fp;
+  float Mh = M[0], Sh = S[0];
+#pragma unroll
+  for (int q = 1; q < H; ++q)
+    if (hh == q) { Mh = M[q]; Sh = S[q]; }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int c = c0; c < c1; ++c) {
+    const float* pr = part + c * stride;
+    acc += reinterpret_cast<const f32x4*>(pr + 16)[k4] * __expf(pr[hh] - Mh);
+  }
+  reinterpret_cast<f32x4*>(zhub + hb * KP)[k4] = acc * (1.0f / (Sh + kSoftmaxEps));
 }
 
-// z = sum_c z_c e^(m_c - M) / (S + eps).  Grid (hubs, KP/64); 64 columns x 4
-// chunk lanes per block.
-__global__ void __launch_bounds__(256) k_hub_merge(const float* __restrict__ part, int Fp,
-                                                   const int32_t* __restrict__ chunk_ptr,
-                                                   const float* __restrict__ hubstat,
-                                                   float* __restrict__ zhub) {
-  __shared__ float sred[256];
-  const int tid = threadIdx.x;
-  const int64_t hb = blockIdx.x;
-  const int KP = H * Fp;
-  const int64_t stride = 16 + KP;
-  const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
-  const int k = blockIdx.y * 64 + (tid & 63);
-  const int cl = tid >> 6;
-  float zsum = 0.f;
-  int hh = 0;
-  if (k < KP) {
-    hh = k / Fp;
-    const float Mh = hubstat[hb * 16 + hh];
-    for (int c = c0 + cl; c < c1; c += 4) {
-      const float* pr = part + c * stride;
-      zsum = fmaf(pr[16 + k], __expf(pr[hh] - Mh), zsum);
-    }
-  }
-  sred[tid] = zsum;
-  __syncthreads();
-  if (cl == 0 && k < KP) {
-    const float zt = sred[tid] + sred[tid + 64] + sred[tid + 128] + sred[tid + 192];
-    zhub[hb * KP + k] = zt / (hubstat[hb * 16 + 8 + hh] + kSoftmaxEps);
-  }
-}
 
 // ---------------------------------------------------------------------------
 inline int kf_for(int F) { return (F + 63) / 64; }
@@ -2338,7 +2346,7 @@ gfd_status launch_stream(const AggArgs& a, const PackLayout& L, int64_t tiles,
 
 template <int KF>
 gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
-  const int Fp = L.Fp, KP = L.KP;
+  const int Fp = L.Fp;
   const gfd_plan& p = a.plan;
   if (p.num_hubs > 0 && (a.stages & GFD_STAGE_HUBS)) {
     int64_t blocks = (p.num_chunks + 3) / 4;
@@ -2346,11 +2354,9 @@ gfd_status launch_aggregate(const AggArgs& a, const PackLayout& L, hipStream_t s
         a.x, a.F, Fp, a.ldx, a.col, a.dst_offset, a.st, a.slope, a.dp, a.seed,
         reinterpret_cast<const int4*>(p.hub_chunk), p.num_chunks, a.part);
     GFD_LAUNCH_CHECK();
-    k_hub_stats<<<int((p.num_hubs + 3) / 4), 256, 0, stream>>>(
-        a.part, Fp, p.hub_chunk_ptr, p.hub_dst, p.num_hubs, a.hubstat, a.stats);
-    GFD_LAUNCH_CHECK();
-    dim3 mg(unsigned(p.num_hubs), unsigned((KP + 63) / 64));
-    k_hub_merge<<<mg, 256, 0, stream>>>(a.part, Fp, p.hub_chunk_ptr, a.hubstat, a.zhub);
+    const int slices = (L.KP / 4 + 63) / 64;
+    k_hub_fin<<<unsigned((p.num_hubs * slices + 3) / 4), 256, 0, stream>>>(
+        a.part, Fp, p.hub_chunk_ptr, p.hub_dst, p.num_hubs, slices, a.stats, a.zhub);
     GFD_LAUNCH_CHECK();
   }
   if (!(a.stages & GFD_STAGE_TILES)) return GFD_OK;
@@ -2483,7 +2489,7 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   PackLayout L = pack_layout(F);
   char* p = static_cast<char*>(packed);
   PackHeader* hdr = reinterpret_cast<PackHeader*>(p + L.hdr_off);
-  k_wmax<<<1, 256, 0, stream>>>(weight, H * C * F, hdr);
+  k_wmax<<<1, 1024, 0, stream>>>(weight, H * C * F, hdr);
   GFD_LAUNCH_CHECK();
   int n_uv = 2 * H * L.Fu;
   k_pack_uv<<<(n_uv + 255) / 256, 256, 0, stream>>>(weight, att_src, att_dst, F, L.Fu,
