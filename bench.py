@@ -168,22 +168,26 @@ def main():
     stream = _lib.stream_handle(dev)
     cplan = plan.cstruct()
 
+    xmax = torch.zeros(1, dtype=torch.float32, device=dev)   # max |x| (one Z-row scale)
+
     def pack_and_logits():
         _lib.call("gfd_gat_pack_weights", W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), F, H, C,
                   packed.data_ptr(), stream)
+        xmax.zero_()
         if world == 1:
-            _lib.call("gfd_gat_logits", x.data_ptr(), N, F, LDX, packed.data_ptr(), H, C,
-                      st.data_ptr(), stream)
+            _lib.call("gfd_gat_logits_ex", x.data_ptr(), N, F, LDX, packed.data_ptr(), H, C,
+                      st.data_ptr(), xmax.data_ptr(), stream)
         else:
             rows = st_hi - st_lo
             if rows > 0:
-                _lib.call("gfd_gat_logits", x[st_lo:].data_ptr(), rows, F, LDX, packed.data_ptr(),
-                          H, C, st_local.data_ptr(), stream)
+                _lib.call("gfd_gat_logits_ex", x[st_lo:].data_ptr(), rows, F, LDX,
+                          packed.data_ptr(), H, C, st_local.data_ptr(), xmax.data_ptr(), stream)
             st.copy_(gdist.all_gather_rows(st_local[:rows], N, world))
+            dist.all_reduce(xmax, op=dist.ReduceOp.MAX)
 
     def aggregate(stage):
-        _lib.call("gfd_gat_aggregate", x.data_ptr(), N, F, LDX, shard.rowptr.data_ptr(),
-                  g.col.data_ptr(), n_dst, lo, st.data_ptr(), packed.data_ptr(),
+        _lib.call("gfd_gat_aggregate_ex", x.data_ptr(), N, F, LDX, shard.rowptr.data_ptr(),
+                  g.col.data_ptr(), n_dst, lo, st.data_ptr(), xmax.data_ptr(), packed.data_ptr(),
                   bias.data_ptr(), H, C, 0.2, 0.0, 0, cplan, stage, out.data_ptr(), None,
                   ws.data_ptr(), ws.numel(), stream)
 

@@ -225,9 +225,11 @@ template <int KSM>
 __global__ void __launch_bounds__(256) k_logits_s(const float* __restrict__ x, int64_t rows,
                                                   int F, int64_t ldx,
                                                   const float* __restrict__ uv, int Fu,
-                                                  float* __restrict__ st) {
+                                                  float* __restrict__ st,
+                                                  float* __restrict__ xmax) {
   const int lane = threadIdx.x & 63;
   const int rl = lane & 15, g = lane >> 4;
+  float am = 0.f;  // max |x| over the values this lane loaded (xmax != NULL)
   const int64_t wave = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   const int64_t nwave = (int64_t(gridDim.x) * blockDim.x) >> 6;
   const int64_t tiles = (rows + 15) / 16;
@@ -262,12 +264,41 @@ __global__ void __launch_bounds__(256) k_logits_s(const float* __restrict__ x, i
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (s < kst) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][u], b[s][u], acc, 0, 0, 0);
+    if (xmax) {  // clamped tail rows repeat row rows - 1: harmless for a max
+#pragma unroll
+      for (int s = 0; s < KSM; ++s)
+        if (s < kst)
+          am = fmaxf(fmaxf(am, fmaxf(fabsf(a[s].x), fabsf(a[s].y))),
+                     fmaxf(fabsf(a[s].z), fabsf(a[s].w)));
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t orow = t * 16 + 4 * g + r;
       if (orow < rows) st[orow * 16 + rl] = acc[r];
     }
   }
+  if (xmax) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+    if (lane == 0)  // non-negative floats order like their bit patterns
+      atomicMax(reinterpret_cast<unsigned int*>(xmax), __float_as_uint(am));
+  }
+}
+
+// max |x| over rows (atomic max into *xmax) for the logits paths that do not
+// fold it in (k_logits<VEC>)
+__global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, int64_t rows, int F,
+                                                int64_t ldx, float* __restrict__ xmax) {
+  float am = 0.f;
+  const int64_t n = rows * int64_t(F);
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r = i / F;
+    am = fmaxf(am, fabsf(x[r * ldx + (i - r * F)]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(xmax), __float_as_uint(am));
 }
 
 // ---------------------------------------------------------------------------
@@ -1715,9 +1746,10 @@ __device__ __forceinline__ float sl_compute(const int4 d, const int j0, const Sl
     if (b + 8 < n) issue(b + 8);
   }
   l = sum_xor8_16_32(l);
-  if (stats && lane < 8) {
-    stats[int64_t(CHK(11, d.x, 1)) * 16 + lane] = m;
-    stats[int64_t(d.x) * 16 + 8 + lane] = l;
+  if (__builtin_expect(stats != nullptr, 0) && lane < 8) {  // training only
+    float* sr = stats + int64_t(CHK(11, d.x, 1)) * 16 + lane;
+    sr[0] = m;
+    sr[8] = l;
   }
   return __builtin_amdgcn_rcpf(l + kSoftmaxEps);
 }
@@ -1745,13 +1777,15 @@ struct SlotZ {
 };
 
 // Aggregate one slot (record from the LDS ring, first batch in q) into registers.
-template <int KF, int PFN>
+// GS: every row takes the scale exponent erg (from max |x|, see k_stream);
+// otherwise the row's own max |z| sets it.
+template <int KF, int PFN, bool GS>
 __device__ __forceinline__ void sl_prep(const SlotRing* __restrict__ ring, const SlotRows<KF, PFN>& q,
                                         const float* __restrict__ x, int64_t ldx, int F, int Fp,
                                         const int32_t* __restrict__ col,
                                         const float* __restrict__ st, float slope, float dp,
                                         uint64_t seed, const float* __restrict__ zhub,
-                                        float* __restrict__ stats, SlotZ<KF>& o,
+                                        float* __restrict__ stats, SlotZ<KF>& o, int erg,
                                         int lane PROF_PARAMS) {
   const int4 d = uni4(ring->d);
   const int j0 = ring->j[lane >> 3];
@@ -1768,21 +1802,24 @@ __device__ __forceinline__ void sl_prep(const SlotRing* __restrict__ ring, const
   f32x2 i2[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) i2[g] = bcast2(inv, 2 * g);
-  float zm = 0.f;
+  int er = erg;
+  if constexpr (!GS) {
+    float zm = 0.f;
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    f32x2 a = {fabsf(z[g][0].x), fabsf(z[g][0].y)};
+    for (int g = 0; g < 4; ++g) {
+      f32x2 a = {fabsf(z[g][0].x), fabsf(z[g][0].y)};
 #pragma unroll
-    for (int qq = 1; qq < KF; ++qq)
-      a = f32x2{fmaxf(a.x, fabsf(z[g][qq].x)), fmaxf(a.y, fabsf(z[g][qq].y))};
-    a *= i2[g];
-    zm = fmaxf(zm, fmaxf(a.x, a.y));
+      for (int qq = 1; qq < KF; ++qq)
+        a = f32x2{fmaxf(a.x, fabsf(z[g][qq].x)), fmaxf(a.y, fabsf(z[g][qq].y))};
+      a *= i2[g];
+      zm = fmaxf(zm, fmaxf(a.x, a.y));
+    }
+    zm = max_wave(zm);
+    int ex = 0;
+    if (zm > 0.f) frexpf(zm, &ex);
+    er = 14 - ex;
+    er = er > 100 ? 100 : (er < -100 ? -100 : er);
   }
-  zm = max_wave(zm);
-  int ex = 0;
-  if (zm > 0.f) frexpf(zm, &ex);
-  int er = 14 - ex;
-  er = er > 100 ? 100 : (er < -100 ? -100 : er);
   const float rs = ldexpf(1.0f, er);
   f32x2 s2[4];
 #pragma unroll
@@ -1831,7 +1868,7 @@ __device__ __forceinline__ void sl_write(const SlotZ<KF>& o, int Fp, _Float16* _
   }
 }
 
-template <int KF, int PFN>
+template <int KF, int PFN, bool GS>
 __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, const SlotRows<KF, PFN>& q,
                                          const float* __restrict__ x, int64_t ldx, int F, int Fp,
                                          const int32_t* __restrict__ col,
@@ -1839,9 +1876,11 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
                                          uint64_t seed, const float* __restrict__ zhub,
                                          float* __restrict__ stats, _Float16* __restrict__ zh,
                                          _Float16* __restrict__ zl, float* __restrict__ rsc,
-                                         int* __restrict__ rid, int r, int lane PROF_PARAMS) {
+                                         int* __restrict__ rid, int r, int erg,
+                                         int lane PROF_PARAMS) {
   SlotZ<KF> o;
-  sl_prep<KF, PFN>(ring, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, o, lane PROF_PASS);
+  sl_prep<KF, PFN, GS>(ring, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats, o, erg,
+                       lane PROF_PASS);
   sl_write<KF>(o, Fp, zh, zl, rsc, rid, r, lane);
 }
 
@@ -1863,7 +1902,7 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
 //    kernel waits on precedes their use (vmcnt is in order).
 //  * Per tile: MFMA -> kh = 1 partials to LDS -> barrier -> kh = 0 waves reduce
 //    and store out; every wave aggregates its next rows into Z -> barrier.
-template <int KF, int KHM, int LO, bool EXACT>
+template <int KF, int KHM, int LO, bool EXACT, bool GS>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
@@ -1871,7 +1910,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
     const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
     uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
-    float* __restrict__ stats, int64_t num_tiles, int mode) {
+    float* __restrict__ stats, const float* __restrict__ xmax, int64_t num_tiles) {
   extern __shared__ __attribute__((aligned(16))) char ssm[];
   const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
   const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
@@ -1897,6 +1936,18 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   // after the first rows are issued
   const float bcol = bias ? bias[ct * 16 + (lane & 15)] : 0.f;
   const float wu = hdr->w_unscale;
+  // GS: one Z-row scale 2^erg for the launch.  Every aggregated row is a convex
+  // combination of x rows (times 1 / (1 - p) under dropout), hub rows included,
+  // so |z| <= max|x| * keep < 2^ex and |z| * 2^erg < 2^14 (fp16 hi and lo' normal
+  // down to 2^-17 of the bound; below that the error stays < 2^-38 max|x|)
+  int erg = 0;
+  if constexpr (GS) {
+    const float bound = *xmax * (dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f);
+    int ex = 0;
+    if (bound > 0.f) frexpf(bound, &ex);
+    erg = 14 - ex;
+    erg = __builtin_amdgcn_readfirstlane(erg > 100 ? 100 : (erg < -100 ? -100 : erg));
+  }
   constexpr int NR = KHM - LO;  // k-steps (of KHM) with W_lo in registers
   f16x8 bh[KHM], bl[NR > 0 ? NR : 1];
 #pragma unroll
@@ -1927,10 +1978,10 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
   if (nv > 0) {
-    sl_store<KF, 4>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
-                 Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, lane PROF_PASS);
-    sl_store<KF, 4>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
-                 Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, lane PROF_PASS);
+    sl_store<KF, 4, GS>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                 Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, erg, lane PROF_PASS);
+    sl_store<KF, 4, GS>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                 Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, erg, lane PROF_PASS);
   }
   __syncthreads();
 
@@ -2034,13 +2085,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       PROF_MARK(8);
 #endif
-      sl_store<KF, 4>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+      sl_store<KF, 4, GS>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                    stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile,
-                   r0, lane PROF_PASS);
+                   r0, erg, lane PROF_PASS);
       PROF_MARK(3);
-      sl_store<KF, 4>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+      sl_store<KF, 4, GS>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
                    stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile,
-                   r1, lane PROF_PASS);
+                   r1, erg, lane PROF_PASS);
       PROF_MARK(4);
     }
     __syncthreads();  // Z of the next tile complete
@@ -2168,7 +2219,7 @@ size_t fused_smem(int Fp) {  // fp16 hi + lo half-tile (= 4 B per element) + par
 int cu_count();
 
 gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const float* uv, int Fu,
-                         float* st, hipStream_t stream) {
+                         float* st, float* xmax, hipStream_t stream) {
   if (rows <= 0) return GFD_OK;
   int64_t blocks = (rows + 63) / 64;  // 4 waves x 16 rows
   if (blocks > 8192) blocks = 8192;
@@ -2179,10 +2230,17 @@ gfd_status launch_logits(const float* x, int64_t rows, int F, int64_t ldx, const
     const int64_t cap = int64_t(cu_count()) * 8;  // resident blocks; grid-stride beyond
     if (nb > cap) nb = cap;
     if (F <= 176)
-      k_logits_s<11><<<int(nb), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
+      k_logits_s<11><<<int(nb), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st, xmax);
     else
-      k_logits_s<16><<<int(nb), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
-  } else if (a % 16 == 0 && ldx % 4 == 0)
+      k_logits_s<16><<<int(nb), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st, xmax);
+    GFD_LAUNCH_CHECK();
+    return GFD_OK;
+  }
+  if (xmax) {
+    k_absmax<<<int(cu_count()) * 4, 256, 0, stream>>>(x, rows, F, ldx, xmax);
+    GFD_LAUNCH_CHECK();
+  }
+  if (a % 16 == 0 && ldx % 4 == 0)
     k_logits<4><<<int(blocks), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
   else if (a % 8 == 0 && ldx % 2 == 0)
     k_logits<2><<<int(blocks), 256, 0, stream>>>(x, rows, F, ldx, uv, Fu, st);
@@ -2243,6 +2301,7 @@ struct AggArgs {
   const float* st; const char* packed; const float* bias; float slope; float dp; uint64_t seed;
   gfd_plan plan; int stages; float* out; float* stats;
   float* part; float* hubstat; float* zhub;
+  const float* xmax;  // max |x| over all rows of x (nullable): one scale for every Z row
 };
 
 constexpr size_t kLdsBytes = 160 * 1024;
@@ -2287,10 +2346,10 @@ gfd_status launch_persist(const AggArgs& a, const PackLayout& L, int64_t tiles,
   return GFD_OK;
 }
 
-template <int KF, int KHM, int LO, bool EXACT>
+template <int KF, int KHM, int LO, bool EXACT, bool GS>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
                            hipStream_t stream) {
-  auto kern = &k_stream<KF, KHM, LO, EXACT>;
+  auto kern = &k_stream<KF, KHM, LO, EXACT, GS>;
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
   const size_t lds = stream_smem(L.Fp, LO);
   if (L.KS / 2 > KHM || lds > kLdsBytes || !a.plan.slot_cols) return GFD_ERR_UNSUPPORTED;
@@ -2319,9 +2378,16 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
-      a.zhub, a.out, a.stats, tiles, fused_mode());
+      a.zhub, a.out, a.stats, a.xmax, tiles);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
+}
+
+template <int KF, int KHM, int LO, bool EXACT>
+gfd_status launch_stream_g(const AggArgs& a, const PackLayout& L, int64_t tiles,
+                           hipStream_t stream) {
+  return a.xmax ? launch_stream_k<KF, KHM, LO, EXACT, true>(a, L, tiles, stream)
+                : launch_stream_k<KF, KHM, LO, EXACT, false>(a, L, tiles, stream);
 }
 
 // k_stream instance for this K: KH = KS / 2 k-steps per wave, at most KHM = 8 / 16 / 21
@@ -2332,14 +2398,14 @@ gfd_status launch_stream(const AggArgs& a, const PackLayout& L, int64_t tiles,
                          hipStream_t stream) {
   const bool exact = L.KS / 2 == (KF == 1 ? 8 : KF == 2 ? 16 : 21);
   if constexpr (KF == 1) {
-    return exact ? launch_stream_k<1, 8, 0, true>(a, L, tiles, stream)
-                 : launch_stream_k<1, 8, 0, false>(a, L, tiles, stream);
+    return exact ? launch_stream_g<1, 8, 0, true>(a, L, tiles, stream)
+                 : launch_stream_g<1, 8, 0, false>(a, L, tiles, stream);
   } else if constexpr (KF == 2) {
-    return exact ? launch_stream_k<2, 16, 0, true>(a, L, tiles, stream)
-                 : launch_stream_k<2, 16, 0, false>(a, L, tiles, stream);
+    return exact ? launch_stream_g<2, 16, 0, true>(a, L, tiles, stream)
+                 : launch_stream_g<2, 16, 0, false>(a, L, tiles, stream);
   } else if constexpr (KF == 3) {
-    return exact ? launch_stream_k<3, 21, 8, true>(a, L, tiles, stream)
-                 : launch_stream_k<3, 21, 8, false>(a, L, tiles, stream);
+    return exact ? launch_stream_g<3, 21, 8, true>(a, L, tiles, stream)
+                 : launch_stream_g<3, 21, 8, false>(a, L, tiles, stream);
   }
   return GFD_ERR_UNSUPPORTED;
 }
@@ -2507,14 +2573,20 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   return GFD_OK;
 }
 
-gfd_status gfd_gat_logits(const float* x, int64_t rows, int F, int64_t ldx, const void* packed,
-                          int heads, int channels, float* st, gfd_stream_t stream_) {
+gfd_status gfd_gat_logits_ex(const float* x, int64_t rows, int F, int64_t ldx,
+                             const void* packed, int heads, int channels, float* st, float* xmax,
+                             gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   if (rows < 0 || (rows > 0 && (!x || !packed || !st)) || ldx < F) return GFD_ERR_ARGUMENT;
   PackLayout L = pack_layout(F);
   const float* uv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + L.uv_off);
-  return launch_logits(x, rows, F, ldx, uv, L.Fu, st, stream);
+  return launch_logits(x, rows, F, ldx, uv, L.Fu, st, xmax, stream);
+}
+
+gfd_status gfd_gat_logits(const float* x, int64_t rows, int F, int64_t ldx, const void* packed,
+                          int heads, int channels, float* st, gfd_stream_t stream_) {
+  return gfd_gat_logits_ex(x, rows, F, ldx, packed, heads, channels, st, nullptr, stream_);
 }
 
 size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int heads,
@@ -2528,15 +2600,17 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int
   s.take<float>(size_t(num_hubs) * L.KP);             // merged hub z rows
   s.take<char>(L.bytes);                              // packed weights (gfd_gat_fwd only)
   s.take<float>(size_t(num_nodes) * 16);              // st (gfd_gat_fwd when st == NULL)
+  s.take<float>(1);                                   // max |x| (gfd_gat_fwd)
   return s.off;
 }
 
-gfd_status gfd_gat_aggregate(const float* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
-                             const int32_t* col, int64_t num_dst, int64_t dst_offset,
-                             const float* st, const void* packed, const float* bias, int heads,
-                             int channels, float slope, float dp, uint64_t seed,
-                             const gfd_plan* plan, int stages, float* out, float* stats, void* ws,
-                             size_t ws_bytes, gfd_stream_t stream_) {
+gfd_status gfd_gat_aggregate_ex(const float* x, int64_t N, int F, int64_t ldx,
+                                const int32_t* rowptr, const int32_t* col, int64_t num_dst,
+                                int64_t dst_offset, const float* st, const float* xmax,
+                                const void* packed, const float* bias, int heads, int channels,
+                                float slope, float dp, uint64_t seed, const gfd_plan* plan,
+                                int stages, float* out, float* stats, void* ws, size_t ws_bytes,
+                                gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   gfd_plan p = plan_or_empty(plan);
@@ -2546,13 +2620,24 @@ gfd_status gfd_gat_aggregate(const float* x, int64_t N, int F, int64_t ldx, cons
   if (num_dst == 0) return GFD_OK;
   PackLayout L = pack_layout(F);
   AggArgs a{x, F, ldx, N, rowptr, col, num_dst, dst_offset, st, static_cast<const char*>(packed),
-            bias, slope, dp, seed, p, stages, out, stats, nullptr, nullptr, nullptr};
+            bias, slope, dp, seed, p, stages, out, stats, nullptr, nullptr, nullptr, xmax};
   if (p.num_hubs > 0) {
     Carve c(ws, ws_bytes);
     hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.hubstat, &a.zhub);
     if (!c.ok) return GFD_ERR_WORKSPACE;
   }
   return aggregate_impl(a, stream);
+}
+
+gfd_status gfd_gat_aggregate(const float* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
+                             const int32_t* col, int64_t num_dst, int64_t dst_offset,
+                             const float* st, const void* packed, const float* bias, int heads,
+                             int channels, float slope, float dp, uint64_t seed,
+                             const gfd_plan* plan, int stages, float* out, float* stats, void* ws,
+                             size_t ws_bytes, gfd_stream_t stream_) {
+  return gfd_gat_aggregate_ex(x, N, F, ldx, rowptr, col, num_dst, dst_offset, st, nullptr, packed,
+                              bias, heads, channels, slope, dp, seed, plan, stages, out, stats,
+                              ws, ws_bytes, stream_);
 }
 
 gfd_status gfd_gat_fwd(const float* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
@@ -2571,17 +2656,20 @@ gfd_status gfd_gat_fwd(const float* x, int64_t N, int F, int64_t ldx, const int3
   PackLayout L = pack_layout(F);
   Carve c(ws, ws_bytes);
   AggArgs a{x, F, ldx, N, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p, GFD_STAGE_ALL,
-            out, stats, nullptr, nullptr, nullptr};
+            out, stats, nullptr, nullptr, nullptr, nullptr};
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.hubstat, &a.zhub);
   void* packed = c.take<char>(L.bytes);
   float* st_ws = c.take<float>(size_t(N) * 16);
+  float* xmax = c.take<float>(1);
   if (!c.ok) return GFD_ERR_WORKSPACE;
   if (st == nullptr) st = st_ws;
   a.st = st;
   a.packed = static_cast<const char*>(packed);
+  a.xmax = xmax;
   s = gfd_gat_pack_weights(weight, att_src, att_dst, F, heads, channels, packed, stream_);
   if (s != GFD_OK) return s;
-  s = gfd_gat_logits(x, N, F, ldx, packed, heads, channels, st, stream_);
+  if (hipMemsetAsync(xmax, 0, sizeof(float), stream) != hipSuccess) return GFD_ERR_HIP;
+  s = gfd_gat_logits_ex(x, N, F, ldx, packed, heads, channels, st, xmax, stream_);
   if (s != GFD_OK) return s;
   return aggregate_impl(a, stream);
 }

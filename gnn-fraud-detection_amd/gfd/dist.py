@@ -117,24 +117,30 @@ def pack_weights(weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Ten
     return packed
 
 
-def shard_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec) -> torch.Tensor:
-    """``[node_hi - node_lo, 16]`` attention logits (s | t) of this rank's node block."""
+def shard_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
+                 xmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``[node_hi - node_lo, 16]`` attention logits (s | t) of this rank's node block.
+    ``xmax`` (optional one-float device tensor) accumulates max |x| over the block
+    (atomic max: start it at 0, reduce it over ranks before the aggregation)."""
     from . import _lib
     from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
     H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
     rows = spec.node_hi - spec.node_lo
     st_local = torch.empty((rows, 2 * H), dtype=torch.float32, device=x.device)
     if rows > 0:
-        _lib.call("gfd_gat_logits", x[spec.node_lo:].data_ptr(), rows, x.size(1), x.stride(0),
-                  packed.data_ptr(), H, C, st_local.data_ptr(), _lib.stream_handle(x.device))
+        _lib.call("gfd_gat_logits_ex", x[spec.node_lo:].data_ptr(), rows, x.size(1),
+                  x.stride(0), packed.data_ptr(), H, C, st_local.data_ptr(), _lib.ptr(xmax),
+                  _lib.stream_handle(x.device))
     return st_local
 
 
 def shard_aggregate(x: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tensor,
                     bias: Optional[torch.Tensor], spec: ShardSpec,
-                    negative_slope: float = 0.2) -> torch.Tensor:
+                    negative_slope: float = 0.2,
+                    xmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``[dst_hi - dst_lo, 64]`` outputs of this rank's destinations, given the
-    all-gathered ``[N, 16]`` logits (gfd_gat_aggregate, hubs + tiles)."""
+    all-gathered ``[N, 16]`` logits (gfd_gat_aggregate_ex, hubs + tiles); with
+    ``xmax`` = max |x| over all rows the tile stage uses one Z-row scale."""
     from . import _lib
     from .graph import _ws
     from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
@@ -149,8 +155,9 @@ def shard_aggregate(x: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tens
     plan = shard.plan
     ws = _ws(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, plan.num_hubs, plan.num_chunks),
              x.device)
-    _lib.call("gfd_gat_aggregate", x.data_ptr(), N, F, x.stride(0), shard.rowptr.data_ptr(),
-              graph.col.data_ptr(), n_dst, spec.dst_lo, st.data_ptr(), packed.data_ptr(),
+    _lib.call("gfd_gat_aggregate_ex", x.data_ptr(), N, F, x.stride(0), shard.rowptr.data_ptr(),
+              graph.col.data_ptr(), n_dst, spec.dst_lo, st.data_ptr(), _lib.ptr(xmax),
+              packed.data_ptr(),
               _lib.ptr(bias), H, C, float(negative_slope), 0.0, 0, plan.cstruct(),
               3, out.data_ptr(), None, ws.data_ptr(), ws.numel(), _lib.stream_handle(x.device))
     return out
@@ -171,9 +178,13 @@ def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torc
     if x.stride(1) != 1:
         raise ValueError("x rows must be contiguous")
     packed = pack_weights(weight, att_src, att_dst)
-    st_local = shard_logits(x, packed, spec)
+    xmax = torch.zeros(1, dtype=torch.float32, device=x.device)
+    st_local = shard_logits(x, packed, spec, xmax)
     st = all_gather_rows(st_local, x.size(0), spec.world, group=group)
-    out = shard_aggregate(x, graph, st, packed, bias, spec, negative_slope)
+    if spec.world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
+    out = shard_aggregate(x, graph, st, packed, bias, spec, negative_slope, xmax)
     if gather_output:
         return all_gather_v_rows(out, spec.dst_bounds, group=group)
     return out

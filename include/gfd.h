@@ -169,6 +169,28 @@ gfd_status gfd_gat_aggregate(const float* x, int64_t num_nodes, int in_features,
                              int stages, float* out, float* stats, void* ws, size_t ws_bytes,
                              gfd_stream_t stream);
 
+/* gfd_gat_logits plus max |x| over the given rows: xmax (nullable, one device
+ * float) is combined with its current value by atomic max, so initialise it to
+ * 0 and, for a row-sharded x, reduce it over the shards (max) before
+ * gfd_gat_aggregate_ex.  Replaces the same PyG GATConv.forward step as
+ * gfd_gat_logits. */
+gfd_status gfd_gat_logits_ex(const float* x, int64_t rows, int in_features, int64_t x_stride,
+                             const void* packed, int heads, int channels, float* st,
+                             float* xmax, gfd_stream_t stream);
+
+/* gfd_gat_aggregate with xmax (nullable) = max |x| over ALL rows of x.  Every
+ * aggregated row is a convex combination of x rows (dropout: times 1/(1-p)),
+ * so the tile stage then uses one power-of-two scale for every Z row instead
+ * of a per-row max (same results within the operator's fp32 tolerance). */
+gfd_status gfd_gat_aggregate_ex(const float* x, int64_t num_nodes, int in_features,
+                                int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                                int64_t num_dst, int64_t dst_offset, const float* st,
+                                const float* xmax, const void* packed, const float* bias,
+                                int heads, int channels, float negative_slope, float dropout_p,
+                                uint64_t dropout_seed, const gfd_plan* plan, int stages,
+                                float* out, float* stats, void* ws, size_t ws_bytes,
+                                gfd_stream_t stream);
+
 /* One-call GATConv forward over the whole graph (num_dst = N, offset 0):
  * pack weights + logits + aggregate.  st (nullable, [N, 2H]) receives the
  * logits; ws must hold gfd_gat_fwd_workspace_size(N, N, F, H, C, hubs, chunks). */

@@ -32,8 +32,9 @@ def _problem(N, E, F, seed, dev):
     return ei, x, W, a_s, a_d, b
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_virtual_ranks_match_oracle(world):
+@pytest.mark.parametrize("world,use_xmax", [(2, False), (3, False), (8, False), (2, True),
+                                            (3, True)])
+def test_virtual_ranks_match_oracle(world, use_xmax):
     from gfd import dist as gdist, graph as ggraph
     dev = torch.device("cuda", 0)
     N, E, F = 20000, 160000, 166
@@ -42,8 +43,13 @@ def test_virtual_ranks_match_oracle(world):
     xd, Wd, asd, add, bd = (t.to(dev) for t in (x, W, a_s, a_d, b))
     packed = gdist.pack_weights(Wd, asd, add)
     specs = [gdist.ShardSpec(g.rowptr, r, world) for r in range(world)]
-    st = torch.cat([gdist.shard_logits(xd, packed, s) for s in specs])
-    out = torch.cat([gdist.shard_aggregate(xd, g, st, packed, bd, s) for s in specs])
+    # use_xmax: the ranks' atomic max|x| accumulated into one tensor (= the
+    # all-reduced value), tile stage with one Z-row scale
+    xmax = torch.zeros(1, device=dev) if use_xmax else None
+    st = torch.cat([gdist.shard_logits(xd, packed, s, xmax) for s in specs])
+    if use_xmax:
+        assert float(xmax) == float(xd.abs().max())
+    out = torch.cat([gdist.shard_aggregate(xd, g, st, packed, bd, s, 0.2, xmax) for s in specs])
     torch.cuda.synchronize()
     expect = ref.gatconv_forward(x, ei, W, a_s, a_d, b, heads=H)
     assert_close(out, expect, what=f"{world} virtual ranks vs oracle")
