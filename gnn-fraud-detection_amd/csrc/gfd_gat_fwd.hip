@@ -1498,6 +1498,14 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
   p.live = slot < num_dst;
 }
 
+// x row j: an unsigned 32 x 32 -> 64-bit product (two scalar multiplies) instead
+// of a sign-extended 64-bit one (the scalar unit is shared by the CU's waves);
+// j >= 0 and 4 * ldx < 2^32 (checked on the host)
+__device__ __forceinline__ float* xrow(const float* x, int j, int64_t ldx) {
+  return reinterpret_cast<float*>(const_cast<char*>(reinterpret_cast<const char*>(x)) +
+                                  uint64_t(uint32_t(j)) * uint64_t(uint32_t(ldx) * 4u));
+}
+
 // Row loads land straight in the destination registers with nothing consuming
 // them here: any use (even a select) in the issuing block would make the
 // compiler wait for the load on the spot.  Lanes f >= F read x[F - 1]; those
@@ -1547,7 +1555,7 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, PFN
   } else {
     constexpr int k = PART - 1;
     const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
-    sl_rows<KF>(x + int64_t(CHK(5, jk, 0)) * ldx, F, lane, q.xv[k]);
+    sl_rows<KF>(xrow(x, CHK(5, jk, 0), ldx), F, lane, q.xv[k]);
   }
 }
 
@@ -1608,7 +1616,7 @@ template <int KF>
 __device__ __forceinline__ void sl_row(const float* __restrict__ x, int64_t ldx, int F, int lane,
                                        int j, bool ok, float (&v)[KF]) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(x) + int64_t(j) * ldx, 0, ok ? F * 4 : 0, 0x00020000);
+      xrow(x, j, ldx), 0, ok ? F * 4 : 0, 0x00020000);
 #pragma unroll
   for (int q = 0; q < KF; ++q)
     v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 256 * q, 0));
@@ -2064,11 +2072,19 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
             pwl[u % AP] = *reinterpret_cast<const f16x8*>(&w);
           }
         }
+#ifdef GFD_MFMA_SPLITACC  // A/B: main product and corrections in separate chains
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[u], acc1, 0, 0, 0);
+#else
         f32x4& acc = (u & 1) ? acc1 : acc0;
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[u], acc, 0, 0, 0);
+#endif
+#ifndef GFD_NO_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);
+#endif
       }
     }
     acc0 += acc1;
@@ -2354,6 +2370,7 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
   const size_t lds = stream_smem(L.Fp, LO);
   if (L.KS / 2 > KHM || lds > kLdsBytes || !a.plan.slot_cols) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
+  if (a.ldx > (int64_t(1) << 29)) return GFD_ERR_UNSUPPORTED;           // xrow: 4 ldx < 2^32
   static size_t attr_lds = 0;  // dynamic LDS the attribute currently allows
   if (lds > attr_lds) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),

@@ -38,6 +38,8 @@ elif VARIANT == "profw":  # prof + a separate wait for the prefetched rows
     FLAGS += ["-DGFD_PROF", "-DGFD_PROF_WAIT"]
 elif VARIANT == "chk":   # bounds-checked k_stream (reports the first bad index instead of faulting)
     FLAGS.append("-DGFD_CHECKED")
+# GFD_EXTRA_FLAGS: A/B builds (e.g. GFD_BUILD_VARIANT=ap1 GFD_EXTRA_FLAGS=-DGFD_STREAM_AP=1)
+FLAGS += os.environ.get("GFD_EXTRA_FLAGS", "").split()
 
 
 def sources():
