@@ -229,7 +229,7 @@ def main():
         buf = (ctypes.c_ulonglong * 32)()
         lib.gfd_debug_prof(buf)
         names = {0: "mfma", 1: "barrier1", 2: "reduce", 8: "wait-rows", 9: "agg-compute",
-                 3: "agg-epilogue0", 4: "agg-epilogue1", 18: "drain", 16: "issue0", 17: "issue1",
+                 3: "agg-epilogue0", 4: "agg-epilogue1", 19: "pair-light", 18: "drain", 16: "issue0", 17: "issue1",
                  5: "records", 6: "barrier2"}
         tot = sum(buf[i] for i in names)
         log("[bench] k_stream phase cycles (summed over waves): " + ", ".join(

@@ -1784,26 +1784,11 @@ struct SlotZ {
   int row;  // destination row (-1: empty slot)
 };
 
-// Aggregate one slot (record from the LDS ring, first batch in q) into registers.
-// GS: every row takes the scale exponent erg (from max |x|, see k_stream);
-// otherwise the row's own max |z| sets it.
-template <int KF, int PFN, bool GS>
-__device__ __forceinline__ void sl_prep(const SlotRing* __restrict__ ring, const SlotRows<KF, PFN>& q,
-                                        const float* __restrict__ x, int64_t ldx, int F, int Fp,
-                                        const int32_t* __restrict__ col,
-                                        const float* __restrict__ st, float slope, float dp,
-                                        uint64_t seed, const float* __restrict__ zhub,
-                                        float* __restrict__ stats, SlotZ<KF>& o, int erg,
-                                        int lane PROF_PARAMS) {
-  const int4 d = uni4(ring->d);
-  const int j0 = ring->j[lane >> 3];
-#ifdef GFD_PROF
-  const uint64_t t_in = __builtin_readcyclecounter();
-#endif
-  f32x2 z[4][KF];
-  const float inv = sl_compute<KF, PFN>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
-                                   stats, lane, z);
-  PROF_MARK(9);
+// Normalise (inv of head lane & 7), scale by 2^er and split into fp16 hi / lo'
+// (GS: er = erg for every row; otherwise from the row's max |z|).
+template <int KF, bool GS>
+__device__ __forceinline__ void sl_pack(const f32x2 (&z)[4][KF], float inv, int erg, int lane,
+                                        SlotZ<KF>& o) {
   // row scale from max |z_h| * inv_h (rounding is monotonic, so this equals the
   // max of the normalised values); normalisation and scale in one multiplier
   // per head pair (inv * 2^er is exact)
@@ -1845,6 +1830,29 @@ __device__ __forceinline__ void sl_prep(const SlotRing* __restrict__ ring, const
     o.lo[qq] = b.v;
   }
   o.er = er;
+}
+
+// Aggregate one slot (record from the LDS ring, first batch in q) into registers.
+// GS: every row takes the scale exponent erg (from max |x|, see k_stream);
+// otherwise the row's own max |z| sets it.
+template <int KF, int PFN, bool GS>
+__device__ __forceinline__ void sl_prep(const SlotRing* __restrict__ ring, const SlotRows<KF, PFN>& q,
+                                        const float* __restrict__ x, int64_t ldx, int F, int Fp,
+                                        const int32_t* __restrict__ col,
+                                        const float* __restrict__ st, float slope, float dp,
+                                        uint64_t seed, const float* __restrict__ zhub,
+                                        float* __restrict__ stats, SlotZ<KF>& o, int erg,
+                                        int lane PROF_PARAMS) {
+  const int4 d = uni4(ring->d);
+  const int j0 = ring->j[lane >> 3];
+#ifdef GFD_PROF
+  const uint64_t t_in = __builtin_readcyclecounter();
+#endif
+  f32x2 z[4][KF];
+  const float inv = sl_compute<KF, PFN>(d, j0, q, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
+                                   stats, lane, z);
+  PROF_MARK(9);
+  sl_pack<KF, GS>(z, inv, erg, lane, o);
   o.row = d.x;
 #ifdef GFD_PROF
   // slot cycles by degree class: 10/11 deg <= 4, 12/13 5..8, 14/15 > 8 (hub rows skipped)
@@ -1874,6 +1882,64 @@ __device__ __forceinline__ void sl_write(const SlotZ<KF>& o, int Fp, _Float16* _
     rsc[r] = ldexpf(1.0f, -o.er);
     rid[r] = o.row;
   }
+}
+
+// z = sum over the first K rows of p_k x_k (no per-message branches: rows past
+// the slot's messages carry p = 0 on valid prefetched rows)
+template <int KF, int K>
+__device__ __forceinline__ void sl_fmaK(f32x2 (&z)[4][KF], const float (&xr)[4][KF], float pv) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    f32x2 p2[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * k + 2 * g);
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq)
+        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
+  }
+}
+
+// A slot with at most 4 messages (all rows prefetched), not a hub, no dropout
+// -- most slots: straight-line code, the softmax sum and reciprocal independent
+// of the FMA block (which has no per-message branches: rows past the slot's
+// messages carry p = 0 on valid prefetched rows).  Same arithmetic as
+// sl_compute + sl_pack.  kmax: messages to run (wave-uniform, >= n).
+template <int KF, bool GS>
+__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, 4>& q, int kmax,
+                                         float slope, int Fp, float* __restrict__ stats,
+                                         _Float16* __restrict__ zh, _Float16* __restrict__ zl,
+                                         float* __restrict__ rsc, int* __restrict__ rid, int r,
+                                         int erg, int lane) {
+  if (d.x < 0) {  // past the last destination
+    if (lane == 0) rid[r] = -1;
+    return;
+  }
+  const int kk = lane >> 3;
+  const int n = d.z - d.y;
+  const float v = leaky01(q.sj + q.th, slope);
+  const float m = max_xor8_16_32(kk < n ? v : -INFINITY);
+  const float p = kk < n ? __expf(v - m) : 0.f;
+  const float l = sum_xor8_16_32(p);
+  if (__builtin_expect(stats != nullptr, 0) && lane < 8) {  // training only
+    float* sr = stats + int64_t(CHK(11, d.x, 1)) * 16 + lane;
+    sr[0] = m;
+    sr[8] = l;
+  }
+  const float inv = __builtin_amdgcn_rcpf(l + kSoftmaxEps);
+  f32x2 z[4][KF];
+  if (kmax <= 1) sl_fmaK<KF, 1>(z, q.xv, p);
+  else if (kmax == 2) sl_fmaK<KF, 2>(z, q.xv, p);
+  else sl_fmaK<KF, 4>(z, q.xv, p);
+  SlotZ<KF> o;
+  sl_pack<KF, GS>(z, inv, erg, lane, o);
+  o.row = d.x;
+  sl_write<KF>(o, Fp, zh, zl, rsc, rid, r, lane);
 }
 
 template <int KF, int PFN, bool GS>
@@ -1910,7 +1976,7 @@ __device__ __forceinline__ void sl_store(const SlotRing* __restrict__ ring, cons
 //    kernel waits on precedes their use (vmcnt is in order).
 //  * Per tile: MFMA -> kh = 1 partials to LDS -> barrier -> kh = 0 waves reduce
 //    and store out; every wave aggregates its next rows into Z -> barrier.
-template <int KF, int KHM, int LO, bool EXACT, bool GS>
+template <int KF, int KHM, int LO, bool EXACT, bool GS, bool LIGHT>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const float* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
@@ -1918,7 +1984,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
     const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
     uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
-    float* __restrict__ stats, const float* __restrict__ xmax, int64_t num_tiles) {
+    float* __restrict__ stats, const float* __restrict__ xmax, int64_t num_tiles,
+    const int64_t* __restrict__ split) {
   extern __shared__ __attribute__((aligned(16))) char ssm[];
   const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
   const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
@@ -1936,9 +2003,12 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   const int64_t G = gridDim.x;
   const int64_t t0 = blockIdx.x;
   // tiles t0 + v*G, v < nv
-  const int64_t nv = t0 < num_tiles ? (num_tiles - 1 - t0) / G + 1 : 0;
+  // LIGHT: tiles [*split, num_tiles) (every slot <= 4 messages, no hub, no
+  // dropout); otherwise [0, *split)
+  const int64_t tb = LIGHT ? *split : 0, te = LIGHT ? num_tiles : *split;
+  const int64_t nv = t0 < te - tb ? (te - tb - 1 - t0) / G + 1 : 0;
   int lane = opaque(threadIdx.x & 63);
-  auto slot = [&](int64_t v, int r) { return (t0 + v * G) * kTile + r; };
+  auto slot = [&](int64_t v, int r) { return (tb + t0 + v * G) * kTile + r; };
 
   // kernel-lifetime constants first: nothing the loop waits on may be loaded
   // after the first rows are issued
@@ -1986,10 +2056,19 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
   if (nv > 0) {
-    sl_store<KF, 4, GS>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
-                 Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, erg, lane PROF_PASS);
-    sl_store<KF, 4, GS>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
-                 Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, erg, lane PROF_PASS);
+    if constexpr (LIGHT) {
+      const int4 da = uni4(ring0[r0].d), db = uni4(ring0[r1].d);
+      const int kmax = max(da.z - da.y, db.z - db.y);
+      sl_light<KF, GS>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0,
+                       r0, erg, lane);
+      sl_light<KF, GS>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0,
+                       r1, erg, lane);
+    } else {
+      sl_store<KF, 4, GS>(ring0 + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                          Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, erg, lane PROF_PASS);
+      sl_store<KF, 4, GS>(ring0 + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                          Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, erg, lane PROF_PASS);
+    }
   }
   __syncthreads();
 
@@ -2101,14 +2180,24 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       PROF_MARK(8);
 #endif
-      sl_store<KF, 4, GS>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
-                   stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile,
-                   r0, erg, lane PROF_PASS);
-      PROF_MARK(3);
-      sl_store<KF, 4, GS>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub,
-                   stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile, rid0 + pn * kTile,
-                   r1, erg, lane PROF_PASS);
-      PROF_MARK(4);
+      if constexpr (LIGHT) {
+        const int4 da = uni4(ring0[pn * kTile + r0].d), db = uni4(ring0[pn * kTile + r1].d);
+        const int kmax = max(da.z - da.y, db.z - db.y);  // wave-uniform
+        sl_light<KF, GS>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS,
+                         rsc0 + pn * kTile, rid0 + pn * kTile, r0, erg, lane);
+        sl_light<KF, GS>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS,
+                         rsc0 + pn * kTile, rid0 + pn * kTile, r1, erg, lane);
+        PROF_MARK(19);
+      } else {
+        sl_store<KF, 4, GS>(ring0 + pn * kTile + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed,
+                            zhub, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile,
+                            rid0 + pn * kTile, r0, erg, lane PROF_PASS);
+        PROF_MARK(3);
+        sl_store<KF, 4, GS>(ring0 + pn * kTile + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed,
+                            zhub, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile,
+                            rid0 + pn * kTile, r1, erg, lane PROF_PASS);
+        PROF_MARK(4);
+      }
     }
     __syncthreads();  // Z of the next tile complete
     PROF_MARK(6);
@@ -2318,6 +2407,7 @@ struct AggArgs {
   gfd_plan plan; int stages; float* out; float* stats;
   float* part; float* hubstat; float* zhub;
   const float* xmax;  // max |x| over all rows of x (nullable): one scale for every Z row
+  int64_t* split;     // device word: first light tile (k_split / k_stream); workspace
 };
 
 constexpr size_t kLdsBytes = 160 * 1024;
@@ -2362,20 +2452,67 @@ gfd_status launch_persist(const AggArgs& a, const PackLayout& L, int64_t tiles,
   return GFD_OK;
 }
 
+// First tile of the light range: tiles run in descending-degree order, so the
+// slots that fit k_stream's light path (<= 4 messages, not a hub) form a
+// suffix; *split = ceil(first light slot / 16) (num_tiles under dropout: the
+// light path has no dropout).  One block narrows the range 1024-fold per pass.
+__global__ void __launch_bounds__(1024) k_split(const int4* __restrict__ desc, int64_t num_dst,
+                                                int64_t num_tiles, float dp,
+                                                int64_t* __restrict__ split) {
+  __shared__ int64_t s_lo, s_hi, s_first;
+  const int t = threadIdx.x;
+  if (dp > 0.f) {
+    if (t == 0) *split = num_tiles;
+    return;
+  }
+  auto light = [&](int64_t s) {
+    if (s >= num_dst) return true;
+    const int4 d = desc[s];
+    return d.w < 0 && d.z - d.y <= 4;
+  };
+  if (t == 0) { s_lo = 0; s_hi = num_dst; }  // answer in [lo, hi]; light(num_dst) holds
+  __syncthreads();
+  for (;;) {
+    const int64_t lo = s_lo, hi = s_hi;
+    const int64_t span = hi - lo;
+    const int64_t step = span <= 1024 ? 1 : (span + 1023) / 1024;
+    if (t == 0) s_first = hi;
+    __syncthreads();
+    const int64_t p = lo + int64_t(t) * step;
+    if (p < hi && light(p)) atomicMin(reinterpret_cast<unsigned long long*>(&s_first),
+                                      (unsigned long long)p);
+    __syncthreads();
+    const int64_t f = s_first;
+    if (step == 1) {
+      if (t == 0) *split = (f + kTile - 1) / kTile;
+      return;
+    }
+    __syncthreads();
+    if (t == 0) {
+      s_hi = f;
+      s_lo = f - step + 1 > lo ? f - step + 1 : lo;
+    }
+    __syncthreads();
+  }
+}
+
 template <int KF, int KHM, int LO, bool EXACT, bool GS>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
                            hipStream_t stream) {
-  auto kern = &k_stream<KF, KHM, LO, EXACT, GS>;
+  auto kheavy = &k_stream<KF, KHM, LO, EXACT, GS, false>;
+  auto klight = &k_stream<KF, KHM, LO, EXACT, GS, true>;
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
   const size_t lds = stream_smem(L.Fp, LO);
-  if (L.KS / 2 > KHM || lds > kLdsBytes || !a.plan.slot_cols) return GFD_ERR_UNSUPPORTED;
+  if (L.KS / 2 > KHM || lds > kLdsBytes || !a.plan.slot_cols || !a.split)
+    return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
   if (a.ldx > (int64_t(1) << 29)) return GFD_ERR_UNSUPPORTED;           // xrow: 4 ldx < 2^32
-  static size_t attr_lds = 0;  // dynamic LDS the attribute currently allows
+  static size_t attr_lds = 0;  // dynamic LDS the attributes currently allow
   if (lds > attr_lds) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)) != hipSuccess)
-      return GFD_ERR_HIP;
+    for (auto kern : {kheavy, klight})
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)) != hipSuccess)
+        return GFD_ERR_HIP;
     attr_lds = lds;
   }
   int64_t grid = cu_count();
@@ -2389,14 +2526,19 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, int64_t tiles,
       return GFD_ERR_HIP;
   }
 #endif
-  kern<<<int(grid), kSWaves * 64, lds, stream>>>(
-      a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
-      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
-      reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
-      reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
-      reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
-      a.zhub, a.out, a.stats, a.xmax, tiles);
+  k_split<<<1, 1024, 0, stream>>>(reinterpret_cast<const int4*>(p.slot_desc), a.num_dst, tiles,
+                                  a.dp, a.split);
   GFD_LAUNCH_CHECK();
+  for (auto kern : {kheavy, klight}) {  // tiles [0, split) general path, [split, tiles) light
+    kern<<<int(grid), kSWaves * 64, lds, stream>>>(
+        a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
+        reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
+        reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
+        reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
+        reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
+        a.zhub, a.out, a.stats, a.xmax, tiles, a.split);
+    GFD_LAUNCH_CHECK();
+  }
   return GFD_OK;
 }
 
@@ -2615,6 +2757,7 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int
   s.take<float>(size_t(num_chunks) * (16 + L.KP));    // hub partials
   s.take<float>(size_t(num_hubs) * 16);               // per-hub (max, sum)
   s.take<float>(size_t(num_hubs) * L.KP);             // merged hub z rows
+  s.take<int64_t>(1);                                 // light-tile split (tile stage)
   s.take<char>(L.bytes);                              // packed weights (gfd_gat_fwd only)
   s.take<float>(size_t(num_nodes) * 16);              // st (gfd_gat_fwd when st == NULL)
   s.take<float>(1);                                   // max |x| (gfd_gat_fwd)
@@ -2637,11 +2780,16 @@ gfd_status gfd_gat_aggregate_ex(const float* x, int64_t N, int F, int64_t ldx,
   if (num_dst == 0) return GFD_OK;
   PackLayout L = pack_layout(F);
   AggArgs a{x, F, ldx, N, rowptr, col, num_dst, dst_offset, st, static_cast<const char*>(packed),
-            bias, slope, dp, seed, p, stages, out, stats, nullptr, nullptr, nullptr, xmax};
-  if (p.num_hubs > 0) {
+            bias, slope, dp, seed, p, stages, out, stats, nullptr, nullptr, nullptr, xmax,
+            nullptr};
+  {
     Carve c(ws, ws_bytes);
     hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.hubstat, &a.zhub);
-    if (!c.ok) return GFD_ERR_WORKSPACE;
+    a.split = c.take<int64_t>(1);
+    if (!c.ok) {
+      if (p.num_hubs > 0) return GFD_ERR_WORKSPACE;
+      a.split = nullptr;  // no room for the split word: general tile path only
+    }
   }
   return aggregate_impl(a, stream);
 }
@@ -2673,8 +2821,9 @@ gfd_status gfd_gat_fwd(const float* x, int64_t N, int F, int64_t ldx, const int3
   PackLayout L = pack_layout(F);
   Carve c(ws, ws_bytes);
   AggArgs a{x, F, ldx, N, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p, GFD_STAGE_ALL,
-            out, stats, nullptr, nullptr, nullptr, nullptr};
+            out, stats, nullptr, nullptr, nullptr, nullptr, nullptr};
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.hubstat, &a.zhub);
+  a.split = c.take<int64_t>(1);
   void* packed = c.take<char>(L.bytes);
   float* st_ws = c.take<float>(size_t(N) * 16);
   float* xmax = c.take<float>(1);
