@@ -1403,6 +1403,9 @@ __global__ void __launch_bounds__(1024, 4) k_pair(
 // ---------------------------------------------------------------------------
 // k_stream and its slot helpers (kernel comment below).
 constexpr int kSWaves = 8;
+#ifndef GFD_STREAM_AP_LIGHT  // the same for the light-tile kernel (fewer live registers)
+#define GFD_STREAM_AP_LIGHT 2
+#endif
 #ifndef GFD_STREAM_AP  // A-fragment k-steps read ahead in the MFMA loop
 #define GFD_STREAM_AP 2
 #endif
@@ -1529,7 +1532,7 @@ __device__ __forceinline__ void sl_rows(const float* __restrict__ xr, int F, int
 // One piece of the issue of a slot's first batch: part 0 = logits (t_i, s_j),
 // the source window and the ring record; part 1 + k = x row k.  The stream
 // kernel spreads the parts over the MFMA k-steps.
-template <int PART, int KF, int PFN>
+template <int PART, int KF, int PFN, bool LIGHT = false>
 __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, PFN>& q,
                                               const float* __restrict__ x, int64_t ldx, int F,
                                               const int32_t* __restrict__ col,
@@ -1546,12 +1549,14 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, PFN
     q.sj = st[int64_t(CHK(4, jm, 0)) * 16 + h];
     // sources of messages 8 .. 71 (one per lane), range-checked: light, hub and
     // empty slots fetch nothing
-    const int nx = (p.live && hw < 0 && e1 - e0 > 8) ? e1 - e0 - 8 : 0;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<int32_t*>(col) + e0 + 8, 0, nx * 4, 0x00020000);
-    q.cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+    if constexpr (!LIGHT) {  // the light path needs neither the window nor the sources
+      const int nx = (p.live && hw < 0 && e1 - e0 > 8) ? e1 - e0 - 8 : 0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int32_t*>(col) + e0 + 8, 0, nx * 4, 0x00020000);
+      q.cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+      if ((lane & 56) == 8) ring->j[lane & 7] = p.v;
+    }
     if (lane == 0) ring->d = make_int4(p.live ? row : -1, e0, e1, hw);
-    if ((lane & 56) == 8) ring->j[lane & 7] = p.v;
   } else {
     constexpr int k = PART - 1;
     const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
@@ -2098,7 +2103,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     // A fragments (and LDS-resident W_lo) AP k-steps ahead; the scheduling
     // barriers keep the compiler from hoisting every LDS read of the tile
     // (registers belong to W)
-    constexpr int AP = GFD_STREAM_AP;
+    constexpr int AP = LIGHT ? GFD_STREAM_AP_LIGHT : GFD_STREAM_AP;
     f16x8 phi[AP], plo[AP], pwl[AP];
 #pragma unroll
     for (int u = 0; u < AP; ++u) {
@@ -2122,20 +2127,20 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       // k-steps: piece i in k-step i * KHM / 10
       SlotRing* rg = ring0 + pn * kTile;
 #define GFD_PIECE(i) (u == (i) * KHM / 10)
-      if (GFD_PIECE(0)) sl_issue_part<0>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
-      if (GFD_PIECE(1)) sl_issue_part<1>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
-      if (GFD_PIECE(2)) sl_issue_part<2>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
-      if (GFD_PIECE(3)) sl_issue_part<3>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(0)) sl_issue_part<0, KF, 4, LIGHT>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(1)) sl_issue_part<1, KF, 4, LIGHT>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(2)) sl_issue_part<2, KF, 4, LIGHT>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+      if (GFD_PIECE(3)) sl_issue_part<3, KF, 4, LIGHT>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
       if (GFD_PIECE(4)) {
-        sl_issue_part<4>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
+        sl_issue_part<4, KF, 4, LIGHT>(n0, d0, x, ldx, F, col, st, dst_offset, rg + r0, lane);
         sl_rec(n0, slot(v + 2, r0), num_dst, desc, cols8, lane);
       }
-      if (GFD_PIECE(5)) sl_issue_part<0>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
-      if (GFD_PIECE(6)) sl_issue_part<1>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
-      if (GFD_PIECE(7)) sl_issue_part<2>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
-      if (GFD_PIECE(8)) sl_issue_part<3>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(5)) sl_issue_part<0, KF, 4, LIGHT>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(6)) sl_issue_part<1, KF, 4, LIGHT>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(7)) sl_issue_part<2, KF, 4, LIGHT>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+      if (GFD_PIECE(8)) sl_issue_part<3, KF, 4, LIGHT>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
       if (GFD_PIECE(9)) {
-        sl_issue_part<4>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
+        sl_issue_part<4, KF, 4, LIGHT>(n1, d1, x, ldx, F, col, st, dst_offset, rg + r1, lane);
         sl_rec(n1, slot(v + 2, r1), num_dst, desc, cols8, lane);
       }
 #undef GFD_PIECE
