@@ -44,13 +44,14 @@ def main():
         wb = write[k] * 1024
         kernels[k] = {"fetch_size_kib_raw": fetch[k], "fetch_bytes": fb, "write_bytes": wb,
                       "hbm_bytes_per_launch": fb + wb}
-    tile = next((k for k in kernels if k.startswith(("k_stream", "k_fused", "k_persist"))), None)
+    # the tile stage is k_split + the k_stream launches (general + light tiles), or k_fused
+    tile = sorted(k for k in kernels if k.startswith(("k_stream", "k_fused", "k_persist", "k_split")))
     entry = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (two passes) {tag}",
              "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 128-B requests at 64 B)",
              "kernels": kernels}
     if tile:
-        entry["tile_kernel"] = tile
-        entry["hbm_bytes_per_launch"] = kernels[tile]["hbm_bytes_per_launch"]
+        entry["tile_kernel"] = " + ".join(tile)
+        entry["hbm_bytes_per_launch"] = sum(kernels[k]["hbm_bytes_per_launch"] for k in tile)
     summary[f"tile:N={N}:E={E}:F={F}:world={world}"] = entry
     json.dump(summary, open(out_path, "w"), indent=1, sort_keys=True)
     for k, v in kernels.items():
