@@ -273,7 +273,8 @@ size_t gfd_gat_bwd_workspace_size(int64_t N, int64_t M, int F, int heads, int ch
   return s.off;
 }
 
-gfd_status gfd_gat_bwd(const float* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
+gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
+                       const int32_t* rowptr,
                        const int32_t* col, const int32_t* colptr, const int32_t* csc_dst,
                        const int32_t* csc_eid, int64_t M, const float* W, const float* att_src,
                        const float* att_dst, int heads, int channels, float slope, float dp,
@@ -282,6 +283,8 @@ gfd_status gfd_gat_bwd(const float* x, int64_t N, int F, int64_t ldx, const int3
                        float* grad_bias, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (heads != H || channels != C || F < 1 || F > 256) return GFD_ERR_UNSUPPORTED;
+  if (x_dtype != GFD_DTYPE_F32) return x_dtype == GFD_DTYPE_BF16 ? GFD_ERR_UNSUPPORTED : GFD_ERR_ARGUMENT;
+  const float* x = static_cast<const float*>(xv);
   if (N <= 0 || M <= 0 || !x || !rowptr || !col || !colptr || !csc_dst || !csc_eid || !W ||
       !att_src || !att_dst || !st || !stats || !g || !grad_W || !grad_as || !grad_ad || ldx < F)
     return GFD_ERR_ARGUMENT;

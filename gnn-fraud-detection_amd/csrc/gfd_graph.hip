@@ -151,19 +151,64 @@ __global__ void k_order_keys(const int32_t* __restrict__ rowptr, int64_t n, int3
 // slot -> {row, e_begin, e_end, hub_rank} and the row's first 8 sources
 // (clamped to the last one): one 16-B + one 32-B load replace the
 // order -> hub_rank -> rowptr -> col chain of dependent loads in the tile kernel.
+// Also the class boundaries of the tile stage (max over slots of 1 + the slot
+// index of every hub / > 4-message slot, and of every hub / > 1-message slot):
+// exact for any slot order.
 __global__ void k_slot_desc(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                             int64_t n, const int32_t* __restrict__ order,
                             const int32_t* __restrict__ hub_rank, int4* __restrict__ desc,
-                            int32_t* __restrict__ cols8) {
+                            int32_t* __restrict__ cols8, int64_t* __restrict__ split) {
+  unsigned long long s_gen = 0, s_light = 0;
   for (int64_t s = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; s < n;
        s += int64_t(gridDim.x) * blockDim.x) {
     const int32_t i = order ? order[s] : int32_t(s);
     const int32_t b = rowptr[i], e = rowptr[i + 1];
-    desc[s] = make_int4(i, b, e, hub_rank ? hub_rank[i] : -1);
+    const int32_t hr = hub_rank ? hub_rank[i] : -1;
+    desc[s] = make_int4(i, b, e, hr);
     if (cols8) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) cols8[s * 8 + k] = col[min(b + k, e - 1)];
     }
+    if (hr >= 0 || e - b > 4) s_gen = (unsigned long long)(s + 1);
+    if (hr >= 0 || e - b > 1) s_light = (unsigned long long)(s + 1);
+  }
+  if (split) {
+    for (int o = 32; o > 0; o >>= 1) {
+      s_gen = max(s_gen, (unsigned long long)__shfl_xor((long long)s_gen, o));
+      s_light = max(s_light, (unsigned long long)__shfl_xor((long long)s_light, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      if (s_gen) atomicMax(reinterpret_cast<unsigned long long*>(split), s_gen);
+      if (s_light) atomicMax(reinterpret_cast<unsigned long long*>(split + 1), s_light);
+    }
+  }
+}
+
+// Two independent 64-bit position-sensitive hashes of a COO edge list (sum of
+// splitmix64 mixes of (position, src, dst); the sum is order-independent in
+// its evaluation, so the block reduction is deterministic in value).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_fingerprint(const int64_t* __restrict__ ei, int64_t E,
+                              unsigned long long* __restrict__ out) {
+  uint64_t a = 0, b = 0;
+  for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < E;
+       e += int64_t(gridDim.x) * blockDim.x) {
+    const uint64_t s = uint64_t(ei[e]), d = uint64_t(ei[E + e]), p = uint64_t(e);
+    a += mix64(p * 0x9E3779B97F4A7C15ull ^ mix64(s + 0x632BE59BD9B4E019ull) ^ (d << 1));
+    b += mix64((s * 0xD6E8FEB86659FD93ull + d) ^ mix64(p + 0x85EBCA77C2B2AE63ull));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += (uint64_t)__shfl_xor((long long)a, o);
+    b += (uint64_t)__shfl_xor((long long)b, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(out, (unsigned long long)a);
+    atomicAdd(out + 1, (unsigned long long)b);
   }
 }
 
@@ -171,13 +216,27 @@ __global__ void k_slot_desc(const int32_t* __restrict__ rowptr, const int32_t* _
 
 extern "C" {
 
+gfd_status gfd_coo_fingerprint(const int64_t* edge_index, int64_t num_edges, uint64_t* out,
+                               gfd_stream_t stream_) {
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (num_edges < 0 || !out || (num_edges > 0 && !edge_index)) return GFD_ERR_ARGUMENT;
+  GFD_HIP_CHECK(hipMemsetAsync(out, 0, 2 * sizeof(uint64_t), stream));
+  if (num_edges == 0) return GFD_OK;
+  k_fingerprint<<<grid_for(num_edges, kBlock, 4096), kBlock, 0, stream>>>(
+      edge_index, num_edges, reinterpret_cast<unsigned long long*>(out));
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
+
 gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t n,
                          const int32_t* order, const int32_t* hub_rank, int32_t* desc,
-                         int32_t* slot_cols, gfd_stream_t stream_) {
+                         int32_t* slot_cols, int64_t* class_split, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (n <= 0 || !rowptr || !desc || (slot_cols && !col)) return GFD_ERR_ARGUMENT;
+  if (class_split) GFD_HIP_CHECK(hipMemsetAsync(class_split, 0, 2 * sizeof(int64_t), stream));
   k_slot_desc<<<grid_for(n), kBlock, 0, stream>>>(rowptr, col, n, order, hub_rank,
-                                                  reinterpret_cast<int4*>(desc), slot_cols);
+                                                  reinterpret_cast<int4*>(desc), slot_cols,
+                                                  class_split);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
@@ -194,7 +253,7 @@ const char* gfd_status_string(gfd_status s) {
   }
 }
 
-int gfd_abi_version(void) { return 1; }
+int gfd_abi_version(void) { return 2; }
 
 static size_t csr_layout(int64_t E, int64_t N, size_t* sort_tmp_out, size_t* scan_tmp_out) {
   size_t sort_tmp = 0, scan_tmp = 0;

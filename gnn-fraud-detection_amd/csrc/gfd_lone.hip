@@ -1,0 +1,181 @@
+// gfd_lone.hip -- destinations whose only message is their own self loop (PyG
+// adds one per node: /root/reference/src/models/gat.py:80 -> GATConv with
+// add_self_loops=True).  Their softmax has one term, alpha = 1 for every head,
+// so PyG's out_i = mean_h W_h x_i + bias = Wbar x_i + bias: K = F instead of
+// 8 F.  A third of the nodes of the C4 power-law graph are lone.
+//
+// k_lone: 4 independent waves per block, each takes 16 lone slots at a time
+// (grid-stride): the 16 rows load straight into the MFMA A layout (lane l:
+// row l & 15, features 32 s + 8 (l >> 4) .. + 7), each row is scaled by a
+// power of two (its max |x| -> [2^13, 2^14)) and split into fp16 hi / lo',
+// out = x . Wbar^T on v_mfma_f32_16x16x32_f16 (3-term split, ~2^-21 relative),
+// Wbar's fragments resident in LDS for the launch.  Not used with dropout
+// (the mask acts per head, so alpha is no longer 1).  Training stats: the
+// softmax max is leaky(s_i + t_i) and the denominator exp(0) = 1.
+#include "gfd_fwd.h"
+
+using namespace gfd;
+using namespace gfd::fwd;
+
+namespace {
+
+constexpr int kLWaves = 4;
+
+// 8 consecutive features f0 .. f0 + 7 of a row as fp32 (zeros past F)
+template <typename XT>
+__device__ __forceinline__ void load8(const typename XT::T* __restrict__ r, int f0, int F,
+                                      float (&v)[8]) {
+  if (f0 + 8 <= F) {
+    if constexpr (XT::kBytes == 4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(r + f0);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(r + f0 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      const uint4 u = *reinterpret_cast<const uint4*>(r + f0);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = f0 + i < F ? xcvt(r[f0 + i]) : 0.f;
+  }
+}
+
+template <typename XT, int KB>
+__global__ void __launch_bounds__(kLWaves * 64) k_lone(
+    const typename XT::T* __restrict__ x, int F, int64_t ldx, int64_t num_dst,
+    int64_t dst_offset, const int4* __restrict__ desc, const float* __restrict__ st,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ wbh,
+    const uint4* __restrict__ wbl, const float* __restrict__ bias, float slope,
+    float* __restrict__ out, float* __restrict__ stats, const int64_t* __restrict__ split) {
+  __shared__ uint4 WB[2][KB][4][64];  // Wbar hi / lo fragments [k-step][col tile][lane]
+  for (int i = threadIdx.x; i < KB * 4 * 64; i += kLWaves * 64) {
+    WB[0][0][0][i] = wbh[i];
+    WB[1][0][0][i] = wbl[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const float wbu = hdr->wb_unscale;
+  float bc[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) bc[ct] = bias ? bias[ct * 16 + r] : 0.f;
+  // lone slots: [16 * ceil(split[1] / 16), num_dst) (the light kernel owns the
+  // rest of its last tile)
+  const int64_t s0 = (split[1] + kTile - 1) / kTile * kTile;
+  const int64_t groups = num_dst > s0 ? (num_dst - s0 + kTile - 1) / kTile : 0;
+  const int64_t wid = (int64_t(blockIdx.x) * kLWaves) + (threadIdx.x >> 6);
+  const int64_t nw = int64_t(gridDim.x) * kLWaves;
+  for (int64_t gi = wid; gi < groups; gi += nw) {
+    const int64_t slot = s0 + gi * kTile + r;
+    const int row = slot < num_dst ? desc[slot].x : -1;
+    float a[KB][8];
+    // the self loop's source is the destination itself: its GLOBAL row of x
+    const typename XT::T* xr = x + (dst_offset + (row < 0 ? 0 : row)) * ldx;
+#pragma unroll
+    for (int s = 0; s < KB; ++s) load8<XT>(xr, 32 * s + 8 * g, row < 0 ? 0 : F, a[s]);
+    float am = 0.f;
+#pragma unroll
+    for (int s = 0; s < KB; ++s)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(a[s][i]));
+    const int er = scale_exp(max_xor16_32(am));  // lanes r, r + 16, r + 32, r + 48
+    const float rs = ldexpf(1.0f, er);
+    f32x4 acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KB; ++s) {
+      union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x2 t = f32x2{a[s][2 * i], a[s][2 * i + 1]} * f32x2{rs, rs};
+        hi.p[i] = __builtin_convertvector(t, f16x2);
+        lo.u[i] = split_lo(t, hi.u[i]);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const uint4 bh = WB[0][s][ct][lane], bl = WB[1][s][ct][lane];
+        const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+        const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, acc[ct], 0, 0, 0);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, acc[ct], 0, 0, 0);
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, acc[ct], 0, 0, 0);
+      }
+    }
+    // accumulator element q of lane l is (row 4 g + q, column ct 16 + r)
+    const float uns = ldexpf(1.0f, -er) * wbu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int src = 4 * g + q;
+      const int orow = __builtin_amdgcn_ds_bpermute(src << 2, row);
+      const float ou = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(uns)));
+      if (orow >= 0) {
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) out[int64_t(orow) * C + ct * 16 + r] = acc[ct][q] * ou + bc[ct];
+      }
+    }
+    if (__builtin_expect(stats != nullptr, 0) && row >= 0) {  // training (no dropout) only
+      // lane (r, g) writes heads g and g + 4 of its row: max = leaky(s + t), sum = 1
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int h = g + 4 * k;
+        const float* sr = st + (dst_offset + row) * 16;
+        stats[int64_t(row) * 16 + h] = leaky(sr[h] + sr[H + h], slope);
+        stats[int64_t(row) * 16 + H + h] = 1.0f;
+      }
+    }
+  }
+}
+
+template <typename XT, int KB>
+gfd_status launch_lone_k(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
+  if (L.KB > KB) return GFD_ERR_UNSUPPORTED;
+  const int64_t groups = (a.num_dst + kTile - 1) / kTile;
+  int64_t grid = int64_t(cu_count()) * 3;
+  if (grid * kLWaves > groups) grid = (groups + kLWaves - 1) / kLWaves;
+  if (grid < 1) grid = 1;
+  const gfd_plan& p = a.plan;
+  k_lone<XT, KB><<<int(grid), kLWaves * 64, 0, stream>>>(
+      static_cast<const typename XT::T*>(a.x), a.F, a.ldx, a.num_dst, a.dst_offset,
+      reinterpret_cast<const int4*>(p.slot_desc), a.st,
+      reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
+      reinterpret_cast<const uint4*>(a.packed + L.wbh_off),
+      reinterpret_cast<const uint4*>(a.packed + L.wbl_off), a.bias, a.slope, a.out, a.stats,
+      p.class_split);
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
+
+template <typename XT>
+gfd_status launch_lone_x(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
+  // KB = ceil(F / 32): instances for F <= 64, 128, 192
+  if (L.KB <= 2) return launch_lone_k<XT, 2>(a, L, stream);
+  if (L.KB <= 4) return launch_lone_k<XT, 4>(a, L, stream);
+  if (L.KB <= 6) return launch_lone_k<XT, 6>(a, L, stream);
+  return GFD_ERR_UNSUPPORTED;
+}
+
+}  // namespace
+
+namespace gfd {
+namespace fwd {
+
+gfd_status launch_lone(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
+  const gfd_plan& p = a.plan;
+  if (!p.slot_desc || !p.class_split || a.dp > 0.f) return GFD_ERR_UNSUPPORTED;
+  // 16-byte row loads: rows aligned to 8 elements of x
+  const uintptr_t base = reinterpret_cast<uintptr_t>(a.x);
+  const int eb = a.xdt == GFD_DTYPE_BF16 ? 2 : 4;
+  if (base % 16 != 0 || (a.ldx * eb) % 16 != 0) return GFD_ERR_UNSUPPORTED;
+  return a.xdt == GFD_DTYPE_BF16 ? launch_lone_x<XBF16>(a, L, stream)
+                                 : launch_lone_x<XF32>(a, L, stream);
+}
+
+}  // namespace fwd
+}  // namespace gfd

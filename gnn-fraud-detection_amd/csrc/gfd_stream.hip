@@ -1,0 +1,393 @@
+// gfd_stream.hip -- light destinations (2..4 messages incl. the self loop):
+// the PyG GATConv.forward softmax-aggregate-project of
+// /root/reference/src/models/gat.py:80 for the bulk of a power-law graph.
+//
+// Weight-stationary streaming tile kernel (persistent, one 8-wave block per
+// CU, two waves per SIMD at up to 256 VGPRs):
+//  * The projection weights stay on chip for the launch: wave w owns column
+//    tile ct = w & 3 over K half kh = w >> 2 (k-steps [kh*KH, kh*KH + KH)):
+//    W_hi of its k-steps in VGPRs, W_lo of the first KH - LO in VGPRs and of
+//    the last LO in LDS.  Only x rows, logits and slot records stream per tile.
+//  * Z goes through LDS once per 16-row tile in the feature-major K order
+//    p = 8 f + h, so a lane stores all 8 heads of its feature with one 16-B
+//    write per (hi, lo).  acc += Zhi.Whi + Zhi.Wlo + Zlo.Whi (lo unscaled).
+//  * Two destinations per wave (rows 2w, 2w+1).  All (at most 4) x rows of a
+//    slot are issued one tile ahead, between the MFMA k-steps of the current
+//    tile; records are loaded two tiles ahead.
+//  * Per tile: MFMA -> kh = 1 partials to LDS -> barrier -> kh = 0 waves reduce
+//    and store out (during the next tile's MFMA); every wave aggregates its
+//    next rows into Z -> barrier.
+//
+// LDS ownership (the invariant every access below keeps):
+//  * ring[par][r] (slot records) is private to the wave that owns slot r
+//    (r = 2w, 2w + 1): written by that wave when it issues tile v + 1 (during
+//    MFMA(v), parity (v + 1) & 1) and read by the same wave after barrier 1 of
+//    iteration v.  The next write of that parity happens at iteration v + 2,
+//    two barriers later.  No other wave touches it.
+//  * Z tile: written after barrier 1 (tile v + 1), read by MFMA(v + 1) after
+//    barrier 2; MFMA(v) reads complete before barrier 1.
+//  * rsc/rid[par]: written with Z (parity of the tile), read by kh = 0 waves in
+//    reduce_store(tile v - 1) during MFMA(v), before barrier 1; the next write
+//    of that parity is after barrier 1 of iteration v.
+//  * red[par]: written by kh = 1 waves after MFMA(v), read by kh = 0 waves
+//    during MFMA(v + 1) (after barriers 1 and 2 of v), next written after
+//    MFMA(v + 2).
+#include "gfd_fwd.h"
+
+using namespace gfd;
+using namespace gfd::fwd;
+
+namespace {
+
+constexpr int kSWaves = 8;
+constexpr int kAP = 2;  // A-fragment k-steps read ahead in the MFMA loop
+
+struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm queue)
+  int v;          // lanes 0..3: {row, e_begin, e_end, hub_rank}; lanes 8..15: sources of
+                  // messages 0..7 (slot_cols); other lanes: row
+  bool live;      // slot < num_dst (otherwise v is a clamped copy, row taken as -1)
+};
+
+template <int KF>
+struct SlotRows {  // a slot's first (and, for light slots, only) batch in flight
+  float th;        // t_i of head lane & 7
+  float sj;        // s_j of the lane's message (lane >> 3)
+  float xv[4][KF];  // x rows of messages 0..3 (lane <-> feature)
+};
+
+__device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst,
+                                       const int4* __restrict__ desc,
+                                       const int32_t* __restrict__ cols8, int lane) {
+  const int64_t sl = slot < num_dst ? slot : num_dst - 1;
+  const int32_t* a = reinterpret_cast<const int32_t*>(desc + sl) + (lane & 3);
+  const int32_t* b = cols8 + sl * 8 + (lane & 7);
+  p.v = *((lane & 56) == 8 ? b : a);  // one dword per lane, one VGPR per slot
+  p.live = slot < num_dst;
+}
+
+// One piece of the issue of a slot: part 0 = logits (t_i, s_j) and the ring
+// record; part 1 + k = x row k.  Issued unconditionally (past the last slot:
+// clamped, ignored records), so no branch joins in-flight loads.
+template <int PART, typename XT, int KF>
+__device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF>& q,
+                                              const void* __restrict__ x, int64_t ldx, int F,
+                                              const float* __restrict__ st, int64_t dst_offset,
+                                              int4* __restrict__ ring, int lane) {
+  if constexpr (PART == 0) {
+    const int h = lane & 7;
+    const int row = __builtin_amdgcn_readlane(p.v, 0);  // >= 0: clamped slots are real rows
+    const int e0 = __builtin_amdgcn_readlane(p.v, 1);
+    const int e1 = __builtin_amdgcn_readlane(p.v, 2);
+    const int hw = __builtin_amdgcn_readlane(p.v, 3);
+    const int jm = __builtin_amdgcn_ds_bpermute((8 + (lane >> 3)) << 2, p.v);  // message lane >> 3
+    q.th = st[(dst_offset + row) * 16 + H + h];
+    q.sj = st[int64_t(jm) * 16 + h];
+    if (lane == 0) *ring = make_int4(p.live ? row : -1, e0, e1, hw);
+  } else {
+    constexpr int k = PART - 1;
+    const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
+    row_regs<XT, KF>(xrow<XT>(x, jk, ldx), F, lane, true, q.xv[k]);
+  }
+}
+
+// z = sum over the first K rows of p_k x_k (no per-message branches: rows past
+// the slot's messages carry p = 0 on valid prefetched rows)
+template <int KF, int K>
+__device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[4][KF], float pv) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    f32x2 p2[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * k + 2 * g);
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq)
+        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
+  }
+}
+
+// A slot with at most 4 messages (all rows prefetched), not a hub, no dropout:
+// straight-line code, the softmax sum and reciprocal independent of the FMA
+// block.  kmax: messages to run (wave-uniform, >= n).
+template <int KF>
+__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF>& q, int kmax,
+                                         float slope, int Fp, float* __restrict__ stats,
+                                         _Float16* __restrict__ zh, _Float16* __restrict__ zl,
+                                         float* __restrict__ rsc, int* __restrict__ rid, int r,
+                                         int erg, int lane) {
+  if (d.x < 0) {  // past the last destination
+    if (lane == 0) rid[r] = -1;
+    return;
+  }
+  const int kk = lane >> 3;
+  const int n = d.z - d.y;
+  const float v = leaky01(q.sj + q.th, slope);
+  const float m = max_xor8_16_32(kk < n ? v : -INFINITY);
+  const float p = kk < n ? __expf(v - m) : 0.f;
+  const float l = sum_xor8_16_32(p);
+  if (__builtin_expect(stats != nullptr, 0) && lane < 8) {  // training only
+    float* sr = stats + int64_t(d.x) * 16 + lane;
+    sr[0] = m;
+    sr[8] = l;
+  }
+  const float inv = __builtin_amdgcn_rcpf(l + kSoftmaxEps);
+  f32x2 z[4][KF];
+  if (kmax <= 1) fma_k<KF, 1>(z, q.xv, p);
+  else if (kmax == 2) fma_k<KF, 2>(z, q.xv, p);
+  else fma_k<KF, 4>(z, q.xv, p);
+  f16x8 hi[KF], lo[KF];
+  const int er = pack_zrow<KF>(z, inv, erg, hi, lo);
+  write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
+  if (lane == 0) {
+    rsc[r] = ldexpf(1.0f, -er);
+    rid[r] = d.x;
+  }
+}
+
+template <typename XT, int KF, int KHM, int LO, bool EXACT>
+__global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
+    const void* __restrict__ x, int F, int Fp, int64_t ldx, int64_t num_dst, int64_t dst_offset,
+    const int4* __restrict__ desc, const int32_t* __restrict__ cols8,
+    const float* __restrict__ st, const PackHeader* __restrict__ hdr,
+    const uint4* __restrict__ wsh, const uint4* __restrict__ wsl, const float* __restrict__ bias,
+    float slope, float* __restrict__ out, float* __restrict__ stats,
+    const float* __restrict__ xmax, const int64_t* __restrict__ split, int to_end) {
+  extern __shared__ __attribute__((aligned(16))) char ssm[];
+  const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
+  const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
+  _Float16* Zh = reinterpret_cast<_Float16*>(ssm);              // [16][ZS]
+  _Float16* Zl = Zh + kTile * ZS;                               // [16][ZS]
+  f32x4* red0 = reinterpret_cast<f32x4*>(Zl + kTile * ZS);      // [2 parity][4 ct][64]
+  int4* ring0 = reinterpret_cast<int4*>(red0 + 2 * 4 * 64);     // [2 parity][16]
+  float* rsc0 = reinterpret_cast<float*>(ring0 + 2 * kTile);    // [2][16] by tile parity
+  int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);         // [2][16]
+  uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);       // [8 waves][LO][64]
+
+  const int wave = wave_uniform(threadIdx.x >> 6);
+  const int ct = wave & 3, kh = wave >> 2;
+  const int r0 = 2 * wave, r1 = r0 + 1;
+  const int64_t G = gridDim.x;
+  const int64_t t0 = blockIdx.x;
+  // light tiles: [ceil(split[0] / 16), ceil(split[1] / 16)) (to_end: up to the
+  // last tile, when k_lone does not run), tiles t0 + v G
+  const int64_t tb = (split[0] + kTile - 1) / kTile;
+  const int64_t te = ((to_end ? num_dst : split[1]) + kTile - 1) / kTile;
+  const int64_t nv = t0 < te - tb ? (te - tb - 1 - t0) / G + 1 : 0;
+  int lane = opaque(threadIdx.x & 63);
+  auto slot = [&](int64_t v, int r) { return (tb + t0 + v * G) * kTile + r; };
+
+  // kernel-lifetime constants first: nothing the loop waits on may be loaded
+  // after the first rows are issued
+  const float bcol = bias ? bias[ct * 16 + (lane & 15)] : 0.f;
+  const float wu = hdr->w_unscale;
+  const int erg = global_scale_exp(xmax, 0.f);
+  constexpr int NR = KHM - LO;  // k-steps (of KHM) with W_lo in registers
+  f16x8 bh[KHM], bl[NR > 0 ? NR : 1];
+#pragma unroll
+  for (int u = 0; u < KHM; ++u) {
+    uint4 vh = make_uint4(0, 0, 0, 0), vl = vh;
+    if (u < KH) {
+      const int idx = ((kh * KH + u) * 4 + ct) * 64 + lane;
+      vh = wsh[idx];
+      vl = wsl[idx];
+    }
+    bh[u] = *reinterpret_cast<const f16x8*>(&vh);
+    if (u < NR) bl[u < NR ? u : 0] = *reinterpret_cast<const f16x8*>(&vl);
+    else WL[(wave * LO + (u - NR)) * 64 + lane] = vl;
+  }
+  if (nv == 0) return;  // uniform per block: no barrier below is reached by anyone
+
+  SlotRec n0, n1;
+  SlotRows<KF> d0, d1;
+  // prologue: tile 0 issued and aggregated; records of tile 1 loading
+  sl_rec(n0, slot(0, r0), num_dst, desc, cols8, lane);
+  sl_rec(n1, slot(0, r1), num_dst, desc, cols8, lane);
+#define GFD_ISSUE(P, n, d, ring) \
+  sl_issue_part<P, XT, KF>(n, d, x, ldx, F, st, dst_offset, ring, lane)
+  GFD_ISSUE(0, n0, d0, ring0 + r0); GFD_ISSUE(1, n0, d0, ring0 + r0);
+  GFD_ISSUE(2, n0, d0, ring0 + r0); GFD_ISSUE(3, n0, d0, ring0 + r0);
+  GFD_ISSUE(4, n0, d0, ring0 + r0);
+  GFD_ISSUE(0, n1, d1, ring0 + r1); GFD_ISSUE(1, n1, d1, ring0 + r1);
+  GFD_ISSUE(2, n1, d1, ring0 + r1); GFD_ISSUE(3, n1, d1, ring0 + r1);
+  GFD_ISSUE(4, n1, d1, ring0 + r1);
+  sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
+  sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
+  {
+    const int4 da = uni4(ring0[r0]), db = uni4(ring0[r1]);
+    const int kmax = max(da.z - da.y, db.z - db.y);
+    sl_light<KF>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, erg,
+                 lane);
+    sl_light<KF>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, erg,
+                 lane);
+  }
+  __syncthreads();
+
+  // out rows of a finished tile (waves kh = 0): own K-half partial + the other
+  // half's from LDS, row scale, bias
+  auto reduce_store = [&](const f32x4& acc, int tpar) {
+    const float* rsc = rsc0 + tpar * kTile;
+    const int* rid = rid0 + tpar * kTile;
+    const f32x4 sum = acc + red0[(tpar * 4 + ct) * 64 + lane];
+    const int n = ct * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (lane >> 4) * 4 + q;
+      const int ri = rid[r];
+      if (ri >= 0) out[int64_t(ri) * C + n] = sum[q] * (rsc[r] * wu) + bcol;
+    }
+  };
+  f32x4 acc_prev = {0.f, 0.f, 0.f, 0.f};  // kh = 0: tile v - 1, stored during MFMA(v)
+  for (int64_t v = 0; v < nv; ++v) {
+    lane = opaque(threadIdx.x & 63);
+    const int par = int(v & 1);
+    // ---- MFMA: out[16 x 16] of column tile ct over K half kh ----
+    const int aoff = (lane & 15) * ZS + 8 * (lane >> 4) + 32 * kh * KH;
+    const _Float16* ah = Zh + aoff;
+    const _Float16* al = Zl + aoff;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    // A fragments (and LDS-resident W_lo) kAP k-steps ahead; the scheduling
+    // barriers keep the compiler from hoisting every LDS read of the tile
+    // (registers belong to W)
+    f16x8 phi[kAP], plo[kAP], pwl[kAP];
+#pragma unroll
+    for (int u = 0; u < kAP; ++u) {
+      phi[u] = *reinterpret_cast<const f16x8*>(ah + 32 * u);
+      plo[u] = *reinterpret_cast<const f16x8*>(al + 32 * u);
+      if (u >= NR) {
+        const uint4 w = WL[(wave * LO + (u - NR)) * 64 + lane];
+        pwl[u] = *reinterpret_cast<const f16x8*>(&w);
+      }
+    }
+    const int pn = par ^ 1;
+    const bool more = v + 1 < nv;
+#pragma unroll
+    for (int u = 0; u < KHM; ++u) {
+      // the next tile's rows are issued between the k-steps (the vector memory
+      // pipe is idle in this phase): 10 pieces (per slot: header, 4 rows)
+      // spread evenly, piece i in k-step i * KHM / 10
+      int4* rg = ring0 + pn * kTile;
+#define GFD_PIECE(i) (u == (i) * KHM / 10)
+      if (GFD_PIECE(0)) GFD_ISSUE(0, n0, d0, rg + r0);
+      if (GFD_PIECE(1)) GFD_ISSUE(1, n0, d0, rg + r0);
+      if (GFD_PIECE(2)) GFD_ISSUE(2, n0, d0, rg + r0);
+      if (GFD_PIECE(3)) GFD_ISSUE(3, n0, d0, rg + r0);
+      if (GFD_PIECE(4)) {
+        GFD_ISSUE(4, n0, d0, rg + r0);
+        sl_rec(n0, slot(v + 2, r0), num_dst, desc, cols8, lane);
+      }
+      if (GFD_PIECE(5)) GFD_ISSUE(0, n1, d1, rg + r1);
+      if (GFD_PIECE(6)) GFD_ISSUE(1, n1, d1, rg + r1);
+      if (GFD_PIECE(7)) GFD_ISSUE(2, n1, d1, rg + r1);
+      if (GFD_PIECE(8)) GFD_ISSUE(3, n1, d1, rg + r1);
+      if (GFD_PIECE(9)) {
+        GFD_ISSUE(4, n1, d1, rg + r1);
+        sl_rec(n1, slot(v + 2, r1), num_dst, desc, cols8, lane);
+      }
+#undef GFD_PIECE
+      if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
+      if (u < KH) {
+        const f16x8 ahi = phi[u % kAP], alo = plo[u % kAP];
+        f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % kAP];
+        if (u + kAP < KH) {
+          phi[u % kAP] = *reinterpret_cast<const f16x8*>(ah + 32 * (u + kAP));
+          plo[u % kAP] = *reinterpret_cast<const f16x8*>(al + 32 * (u + kAP));
+          if (u + kAP >= NR) {
+            const uint4 w = WL[(wave * LO + (u + kAP - NR)) * 64 + lane];
+            pwl[u % kAP] = *reinterpret_cast<const f16x8*>(&w);
+          }
+        }
+        f32x4& acc = (u & 1) ? acc1 : acc0;
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[u], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    acc0 += acc1;
+    if (kh) red0[(par * 4 + ct) * 64 + lane] = acc0;
+    acc_prev = acc0;
+    __syncthreads();  // partials visible; every Z read of this tile done
+
+    // ---- tile v + 1: aggregate its rows into Z ----
+    if (more) {
+      const int4 da = uni4(ring0[pn * kTile + r0]), db = uni4(ring0[pn * kTile + r1]);
+      const int kmax = max(da.z - da.y, db.z - db.y);  // wave-uniform
+      sl_light<KF>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile,
+                   rid0 + pn * kTile, r0, erg, lane);
+      sl_light<KF>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile,
+                   rid0 + pn * kTile, r1, erg, lane);
+    }
+    __syncthreads();  // Z of the next tile complete
+  }
+#undef GFD_ISSUE
+  if (!kh) reduce_store(acc_prev, int((nv - 1) & 1));  // last tile
+}
+
+size_t stream_smem(int Fp, int lo) {
+  return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 2 * 4 * 64 +
+         sizeof(int4) * 2 * kTile + sizeof(float) * 4 * kTile +
+         sizeof(uint4) * kSWaves * lo * 64;
+}
+
+template <typename XT, int KF, int KHM, int LO, bool EXACT>
+gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
+                           hipStream_t stream) {
+  auto kern = &k_stream<XT, KF, KHM, LO, EXACT>;
+  if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
+  const size_t lds = stream_smem(L.Fp, LO);
+  if (L.KS / 2 > KHM || lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;
+  if (!ensure_lds(reinterpret_cast<const void*>(kern), lds)) return GFD_ERR_HIP;
+  const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
+  int64_t grid = cu_count();
+  if (grid > tiles) grid = tiles;
+  const gfd_plan& p = a.plan;
+  kern<<<int(grid), kSWaves * 64, lds, stream>>>(
+      a.x, a.F, L.Fp, a.ldx, a.num_dst, a.dst_offset, reinterpret_cast<const int4*>(p.slot_desc),
+      p.slot_cols, a.st, reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
+      reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
+      reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.out, a.stats,
+      a.xmax, p.class_split, to_end ? 1 : 0);
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
+
+// Instance for this K: KH = KS / 2 k-steps per wave, at most KHM = 8 / 16 / 21
+// for one / two / three feature chunks (F <= 64 / 128 / 168).  KF = 3 keeps
+// W_lo of 8 k-steps per wave in LDS.
+template <typename XT>
+gfd_status launch_stream_x(const AggArgs& a, const PackLayout& L, bool to_end,
+                           hipStream_t stream) {
+  const int KF = kf_for(a.F);
+  const bool exact = L.KS / 2 == (KF == 1 ? 8 : KF == 2 ? 16 : 21);
+  switch (KF) {
+    case 1: return exact ? launch_stream_k<XT, 1, 8, 0, true>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 1, 8, 0, false>(a, L, to_end, stream);
+    case 2: return exact ? launch_stream_k<XT, 2, 16, 0, true>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 2, 16, 0, false>(a, L, to_end, stream);
+    case 3: return exact ? launch_stream_k<XT, 3, 21, 8, true>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 3, 21, 8, false>(a, L, to_end, stream);
+    default: return GFD_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace
+
+namespace gfd {
+namespace fwd {
+
+gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
+                        hipStream_t stream) {
+  const gfd_plan& p = a.plan;
+  if (!p.slot_desc || !p.slot_cols || !p.class_split || a.dp > 0.f) return GFD_ERR_UNSUPPORTED;
+  if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
+  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16>(a, L, to_end, stream)
+                                 : launch_stream_x<XF32>(a, L, to_end, stream);
+}
+
+}  // namespace fwd
+}  // namespace gfd

@@ -23,8 +23,23 @@ P = ct.c_void_p
 
 class GfdPlan(ct.Structure):
     """``gfd_plan`` (include/gfd.h)."""
-    _fields_ = [("row_order", P), ("slot_desc", P), ("slot_cols", P), ("hub_rank", P), ("hub_chunk", P), ("hub_chunk_ptr", P),
-                ("hub_dst", P), ("num_hubs", c_i64), ("num_chunks", c_i64)]
+    _fields_ = [("row_order", P), ("slot_desc", P), ("slot_cols", P), ("hub_rank", P),
+                ("hub_chunk", P), ("hub_chunk_ptr", P), ("hub_dst", P), ("class_split", P),
+                ("num_hubs", c_i64), ("num_chunks", c_i64)]
+
+
+# element types of x (GFD_DTYPE_*)
+DTYPE_F32, DTYPE_BF16 = 0, 1
+
+
+def x_dtype_code(t) -> int:
+    """GFD_DTYPE_* of a feature tensor (fp32 or bf16); raises for anything else."""
+    import torch
+    if t.dtype == torch.float32:
+        return DTYPE_F32
+    if t.dtype == torch.bfloat16:
+        return DTYPE_BF16
+    raise TypeError(f"gfd: node features must be float32 or bfloat16 (got {t.dtype})")
 
 
 PLAN = ct.POINTER(GfdPlan)
@@ -35,6 +50,7 @@ SIGNATURES = {
     "gfd_abi_version": (ct.c_int, []),
     "gfd_csr_workspace_size": (c_sz, [c_i64, c_i64]),
     "gfd_csr_from_coo": (c_i32, [P, c_i64, c_i64, P, P, P, c_sz, P]),
+    "gfd_coo_fingerprint": (c_i32, [P, c_i64, P, P]),
     "gfd_csc_workspace_size": (c_sz, [c_i64, c_i64]),
     "gfd_csc_from_csr": (c_i32, [P, P, c_i64, c_i64, P, P, P, P, c_sz, P]),
     "gfd_plan_workspace_size": (c_sz, [c_i64]),
@@ -42,24 +58,26 @@ SIGNATURES = {
                               ct.POINTER(c_i64), ct.POINTER(c_i64), P, c_sz, P]),
     "gfd_order_workspace_size": (c_sz, [c_i64, c_i32]),
     "gfd_plan_order": (c_i32, [P, c_i64, c_i32, P, P, c_sz, P]),
-    "gfd_plan_desc": (c_i32, [P, P, c_i64, P, P, P, P, P]),
+    "gfd_plan_desc": (c_i32, [P, P, c_i64, P, P, P, P, P, P]),
     "gfd_gat_packed_size": (c_sz, [ct.c_int, ct.c_int, ct.c_int]),
     "gfd_gat_pack_weights": (c_i32, [P, P, P, ct.c_int, ct.c_int, ct.c_int, P, P]),
-    "gfd_gat_logits": (c_i32, [P, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),
-    "gfd_gat_logits_ex": (c_i32, [P, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P, P]),
+    "gfd_gat_logits": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),
+    "gfd_gat_logits_ex": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P,
+                                  P, P]),
     "gfd_gat_fwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int, c_i64,
                                           c_i64]),
-    "gfd_gat_aggregate": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P, P, P,
-                                  ct.c_int, ct.c_int, c_f32, c_f32, c_u64, PLAN, ct.c_int, P, P,
-                                  P, c_sz, P]),
-    "gfd_gat_aggregate_ex": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P, P, P, P,
-                                     ct.c_int, ct.c_int, c_f32, c_f32, c_u64, PLAN, ct.c_int, P,
-                                     P, P, c_sz, P]),
-    "gfd_gat_fwd": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int, ct.c_int,
-                            c_f32, c_f32, c_u64, PLAN, P, P, P, P, c_sz, P]),
+    "gfd_gat_aggregate": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P, P,
+                                  P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, PLAN, ct.c_int, P,
+                                  P, P, c_sz, P]),
+    "gfd_gat_aggregate_ex": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P,
+                                     P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, PLAN,
+                                     ct.c_int, P, P, P, c_sz, P]),
+    "gfd_gat_fwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,
+                            ct.c_int, c_f32, c_f32, c_u64, PLAN, P, P, P, P, c_sz, P]),
     "gfd_gat_bwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int]),
-    "gfd_gat_bwd": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, P, ct.c_int,
-                            ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, P, P, P, P, P, c_sz, P]),
+    "gfd_gat_bwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, P,
+                            ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, P, P, P, P, P,
+                            c_sz, P]),
 }
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "edge index out of range", 3: "workspace too small",

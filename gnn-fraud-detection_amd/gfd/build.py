@@ -20,9 +20,11 @@ ROOT = os.path.dirname(PKG)                       # gnn-fraud-detection_amd/
 REPO = os.path.dirname(ROOT)
 CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
-# GFD_BUILD_VARIANT=prof: diagnostic build (-DGFD_PROF, phase cycle counters) into
-# libgfd_prof.so / build/obj_prof; the product library is untouched.
+# GFD_BUILD_VARIANT=<name>: a diagnostic / A-B build (with GFD_EXTRA_FLAGS) into
+# libgfd_<name>.so / build/obj_<name>; the product library is untouched.
 VARIANT = os.environ.get("GFD_BUILD_VARIANT", "")
+if os.environ.get("GFD_EXTRA_FLAGS") and not VARIANT:
+    raise RuntimeError("GFD_EXTRA_FLAGS needs GFD_BUILD_VARIANT (never rebuild libgfd.so with A/B flags)")
 LIB = os.path.join(PKG, f"libgfd_{VARIANT}.so" if VARIANT else "libgfd.so")
 OBJDIR = os.path.join(ROOT, "build", f"obj_{VARIANT}" if VARIANT else "obj")
 ARCH = os.environ.get("GFD_OFFLOAD_ARCH", "gfx950")
@@ -32,14 +34,12 @@ HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-fno-honor-nans",
          f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
-if VARIANT == "prof":
-    FLAGS.append("-DGFD_PROF")
-elif VARIANT == "profw":  # prof + a separate wait for the prefetched rows
-    FLAGS += ["-DGFD_PROF", "-DGFD_PROF_WAIT"]
-elif VARIANT == "chk":   # bounds-checked k_stream (reports the first bad index instead of faulting)
-    FLAGS.append("-DGFD_CHECKED")
-# GFD_EXTRA_FLAGS: A/B builds (e.g. GFD_BUILD_VARIANT=ap1 GFD_EXTRA_FLAGS=-DGFD_STREAM_AP=1)
+# GFD_EXTRA_FLAGS: A/B builds into their own library (with GFD_BUILD_VARIANT)
 FLAGS += os.environ.get("GFD_EXTRA_FLAGS", "").split()
+# Per-source flags.  k_mid runs 16 waves at <= 128 VGPRs: the SLP vectoriser's
+# packed-pair copies of the gathered rows push it into scratch (rows spilled
+# right after their loads), scalar FMAs with SGPR-broadcast weights do not.
+SOURCE_FLAGS = {"gfd_mid.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():
@@ -57,7 +57,7 @@ def _compile(src: str) -> str:
     newest = max(os.path.getmtime(p) for p in [src] + _deps())
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest:
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *SOURCE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")

@@ -128,9 +128,9 @@ def shard_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
     rows = spec.node_hi - spec.node_lo
     st_local = torch.empty((rows, 2 * H), dtype=torch.float32, device=x.device)
     if rows > 0:
-        _lib.call("gfd_gat_logits_ex", x[spec.node_lo:].data_ptr(), rows, x.size(1),
-                  x.stride(0), packed.data_ptr(), H, C, st_local.data_ptr(), _lib.ptr(xmax),
-                  _lib.stream_handle(x.device))
+        _lib.call("gfd_gat_logits_ex", x[spec.node_lo:].data_ptr(), _lib.x_dtype_code(x), rows,
+                  x.size(1), x.stride(0), packed.data_ptr(), H, C, st_local.data_ptr(),
+                  _lib.ptr(xmax), _lib.stream_handle(x.device))
     return st_local
 
 
@@ -151,11 +151,12 @@ def shard_aggregate(x: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tens
     out = torch.empty((n_dst, C), dtype=torch.float32, device=x.device)
     if n_dst == 0:
         return out
-    shard = graph.shard(spec.dst_lo, spec.dst_hi)
+    shard = graph.shard(spec.dst_lo, spec.dst_hi)   # plan built once per range, cached
     plan = shard.plan
     ws = _ws(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, plan.num_hubs, plan.num_chunks),
              x.device)
-    _lib.call("gfd_gat_aggregate_ex", x.data_ptr(), N, F, x.stride(0), shard.rowptr.data_ptr(),
+    _lib.call("gfd_gat_aggregate_ex", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+              shard.rowptr.data_ptr(),
               graph.col.data_ptr(), n_dst, spec.dst_lo, st.data_ptr(), _lib.ptr(xmax),
               packed.data_ptr(),
               _lib.ptr(bias), H, C, float(negative_slope), 0.0, 0, plan.cstruct(),

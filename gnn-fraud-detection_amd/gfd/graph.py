@@ -5,17 +5,24 @@ dataset.py:104) and PyG rebuilds the self-loop-normalised edge list on every
 call and every layer (remove_self_loops + add_self_loops inside
 GATConv.forward).  Here the CSR (int32 ``rowptr[N+1]`` / ``col[E']``, loops
 removed then one appended per node, duplicates kept, stable order) is built
-once on the GPU by ``gfd_csr_from_coo`` and cached per
-``(edge_index storage, version, N)``; the source-sorted CSC view used by the
-backward and the hub plan (rows with more than ``hub_threshold`` messages are
-split into chunks) are derived lazily from it.
+once on the GPU by ``gfd_csr_from_coo`` and cached; the source-sorted CSC view
+used by the backward, the execution plan (tile order, hub split, class
+boundaries) and destination shards are derived lazily from it and cached on it.
+
+Cache keys (``get_graph``): the tensor object itself (fast path, weakly held)
+and, for a different tensor with the same contents -- the reference moves the
+whole graph to the device every epoch (``batch.to(device)``, train.py:105) --
+a 128-bit device-side fingerprint of ``edge_index`` (``gfd_coo_fingerprint``),
+so the unmodified training loop builds CSR, plan and CSC once.
 """
 from __future__ import annotations
 
 import os
+import threading
 import weakref
+from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -32,7 +39,8 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 @dataclass
 class Plan:
     """Execution plan of one destination range (``gfd_plan``): the tile order
-    (destinations by descending message count) and the hub split."""
+    (destinations by descending message count), the hub split and the slot
+    class boundaries (``class_split``: first light slot, first lone slot)."""
     num_dst: int
     row_order: Optional[torch.Tensor]
     slot_desc: Optional[torch.Tensor]
@@ -43,6 +51,7 @@ class Plan:
     hub_dst: Optional[torch.Tensor]
     num_hubs: int
     num_chunks: int
+    class_split: Optional[torch.Tensor] = None
     _c: object = field(default=None, repr=False)
 
     def cstruct(self):
@@ -54,8 +63,8 @@ class Plan:
                                    p(self.hub_rank) if hubs else None,
                                    p(self.hub_chunk) if hubs else None,
                                    p(self.hub_chunk_ptr) if hubs else None,
-                                   p(self.hub_dst) if hubs else None, self.num_hubs,
-                                   self.num_chunks)
+                                   p(self.hub_dst) if hubs else None, p(self.class_split),
+                                   self.num_hubs, self.num_chunks)
         return _lib.ct.byref(self._c)
 
     def hub_messages(self) -> int:
@@ -64,12 +73,23 @@ class Plan:
         ck = self.hub_chunk.view(-1, 4)
         return int((ck[:, 2] - ck[:, 1]).sum().item())
 
+    def classes(self) -> Tuple[int, int]:
+        """(first light slot, first lone slot) on the host (syncs)."""
+        if self.class_split is None:
+            return self.num_dst, self.num_dst
+        a, b = self.class_split.tolist()
+        return int(a), int(b)
+
 
 def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
                chunk: int = HUB_CHUNK, order: bool = True,
-               col: Optional[torch.Tensor] = None) -> Plan:
+               col: Optional[torch.Tensor] = None, order_cap: Optional[int] = None) -> Plan:
     """Plan for the destination range described by ``rowptr`` ([n+1] int32,
-    absolute positions into ``col``)."""
+    absolute positions into ``col``).  With ``col`` the plan carries the slot
+    sources and class boundaries that the class-scheduled tile stage needs;
+    the boundaries are exact for any ``order`` (gfd_plan_desc), including no
+    order and an order whose degree cap (``order_cap``, default the hub
+    threshold) merges classes."""
     n = rowptr.numel() - 1
     dev = rowptr.device
     lib = _lib.load()
@@ -80,33 +100,32 @@ def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THR
     hub_chunk = torch.empty(4 * max_chunks, dtype=torch.int32, device=dev)
     hub_chunk_ptr = torch.empty(max_hubs + 1, dtype=torch.int32, device=dev)
     hub_dst = torch.empty(max_hubs, dtype=torch.int32, device=dev)
-    ws = _ws(lib.gfd_plan_workspace_size(n), dev)
     nh, nc = _lib.c_i64(0), _lib.c_i64(0)
-    _lib.call("gfd_plan_hubs", rowptr.data_ptr(), n, threshold, chunk, hub_rank.data_ptr(),
-              hub_chunk.data_ptr(), hub_chunk_ptr.data_ptr(), hub_dst.data_ptr(), max_hubs,
-              max_chunks, _lib.ct.byref(nh), _lib.ct.byref(nc), ws.data_ptr(), ws.numel(), stream)
+    if n > 0:
+        ws = _ws(lib.gfd_plan_workspace_size(n), dev)
+        _lib.call("gfd_plan_hubs", rowptr.data_ptr(), n, threshold, chunk, hub_rank.data_ptr(),
+                  hub_chunk.data_ptr(), hub_chunk_ptr.data_ptr(), hub_dst.data_ptr(), max_hubs,
+                  max_chunks, _lib.ct.byref(nh), _lib.ct.byref(nc), ws.data_ptr(), ws.numel(),
+                  stream)
     row_order = None
     if order and n > 0:
         row_order = torch.empty(n, dtype=torch.int32, device=dev)
-        ws = _ws(lib.gfd_order_workspace_size(n, threshold), dev)
-        _lib.call("gfd_plan_order", rowptr.data_ptr(), n, threshold, row_order.data_ptr(),
+        cap = threshold if order_cap is None else order_cap
+        ws = _ws(lib.gfd_order_workspace_size(n, cap), dev)
+        _lib.call("gfd_plan_order", rowptr.data_ptr(), n, cap, row_order.data_ptr(),
                   ws.data_ptr(), ws.numel(), stream)
-    slot_desc = slot_cols = None
+    slot_desc = slot_cols = class_split = None
     if n > 0:
         slot_desc = torch.empty(4 * n, dtype=torch.int32, device=dev)
         if col is not None:
             slot_cols = torch.empty(8 * n, dtype=torch.int32, device=dev)
+            class_split = torch.empty(2, dtype=torch.int64, device=dev)
         _lib.call("gfd_plan_desc", rowptr.data_ptr(), _lib.ptr(col), n, _lib.ptr(row_order),
                   hub_rank.data_ptr() if nh.value > 0 else None, slot_desc.data_ptr(),
-                  _lib.ptr(slot_cols), stream)
+                  _lib.ptr(slot_cols), _lib.ptr(class_split), stream)
     return Plan(n, row_order, slot_desc, slot_cols, hub_rank, hub_chunk[:4 * nc.value],
-                hub_chunk_ptr[:nh.value + 1], hub_dst[:nh.value], nh.value, nc.value)
-
-
-# backwards-compatible name
-def plan_hubs(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
-              chunk: int = HUB_CHUNK) -> Plan:
-    return build_plan(rowptr, num_messages, threshold, chunk)  # no slot_cols
+                hub_chunk_ptr[:nh.value + 1], hub_dst[:nh.value], nh.value, nc.value,
+                class_split)
 
 
 @dataclass
@@ -126,6 +145,7 @@ class CSRGraph:
     num_input_edges: int
     _plan: Optional[Plan] = field(default=None, repr=False)
     _csc: Optional[CSC] = field(default=None, repr=False)
+    _shards: Dict[Tuple[int, int], "CSRShard"] = field(default_factory=dict, repr=False)
 
     @property
     def device(self):
@@ -150,10 +170,16 @@ class CSRGraph:
         return self._csc
 
     def shard(self, lo: int, hi: int) -> "CSRShard":
-        """Destination range [lo, hi): a rowptr view (absolute positions into col)."""
-        rp = self.rowptr[lo:hi + 1]
-        m = int(self.rowptr[hi].item()) - int(self.rowptr[lo].item())
-        return CSRShard(self, lo, hi, rp, m, build_plan(rp, m, col=self.col))
+        """Destination range [lo, hi): a rowptr view (absolute positions into
+        col) and its own plan, built once per range and cached here."""
+        key = (int(lo), int(hi))
+        sh = self._shards.get(key)
+        if sh is None:
+            rp = self.rowptr[lo:hi + 1]
+            m = int(self.rowptr[hi].item()) - int(self.rowptr[lo].item())
+            sh = CSRShard(self, lo, hi, rp, m, build_plan(rp, m, col=self.col))
+            self._shards[key] = sh
+        return sh
 
 
 @dataclass
@@ -189,18 +215,52 @@ def csr_from_coo(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
     return CSRGraph(num_nodes, rowptr, col[:M], M, E)
 
 
-_CACHE: dict = {}
+def fingerprint(edge_index: torch.Tensor) -> Tuple[int, int]:
+    """128-bit content fingerprint of a device COO edge list (one sync)."""
+    ei = edge_index.to(torch.int64).contiguous()
+    out = torch.empty(2, dtype=torch.int64, device=ei.device)
+    _lib.call("gfd_coo_fingerprint", ei.data_ptr(), ei.size(1), out.data_ptr(),
+              _lib.stream_handle(ei.device))
+    a, b = out.tolist()
+    return int(a), int(b)
+
+
+_LOCK = threading.Lock()
+_BY_ID: dict = {}                      # id(edge_index) -> (weakref, key, graph)
+_BY_FP: "OrderedDict" = OrderedDict()  # (device, N, shape, fingerprint) -> graph
+_FP_CAP = 8
 
 
 def get_graph(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
-    """Cached ``csr_from_coo`` keyed on the tensor object (held weakly), its
-    in-place version counter, storage pointer, shape and N."""
+    """Cached ``csr_from_coo``.  Fast path: the same tensor object (held
+    weakly; its in-place version counter, storage pointer, shape and N are
+    part of the key).  Otherwise the content fingerprint: an equal edge list
+    in a new tensor reuses the CSR (and its plan / CSC) built for the first."""
     key = (edge_index._version, int(num_nodes), edge_index.data_ptr(), tuple(edge_index.shape))
-    ent = _CACHE.get(id(edge_index))
-    if ent is not None and ent[0]() is edge_index and ent[1] == key:
-        return ent[2]
-    g = csr_from_coo(edge_index, num_nodes)
+    with _LOCK:
+        ent = _BY_ID.get(id(edge_index))
+        if ent is not None and ent[0]() is edge_index and ent[1] == key:
+            return ent[2]
+    fkey = (str(edge_index.device), int(num_nodes), tuple(edge_index.shape),
+            fingerprint(edge_index))
+    with _LOCK:
+        g = _BY_FP.get(fkey)
+        if g is not None:
+            _BY_FP.move_to_end(fkey)
+    if g is None:
+        g = csr_from_coo(edge_index, num_nodes)
+        with _LOCK:
+            _BY_FP[fkey] = g
+            while len(_BY_FP) > _FP_CAP:
+                _BY_FP.popitem(last=False)
     oid = id(edge_index)
-    ref = weakref.ref(edge_index, lambda _r, oid=oid: _CACHE.pop(oid, None))
-    _CACHE[oid] = (ref, key, g)
+    ref = weakref.ref(edge_index, lambda _r, oid=oid: _BY_ID.pop(oid, None))
+    with _LOCK:
+        _BY_ID[oid] = (ref, key, g)
     return g
+
+
+def clear_cache() -> None:
+    with _LOCK:
+        _BY_ID.clear()
+        _BY_FP.clear()

@@ -27,13 +27,19 @@ SUPPORTED_HEADS = 8
 SUPPORTED_CHANNELS = 64
 
 
-def _check_tensor(name: str, t: torch.Tensor, device):
+def _check_tensor(name: str, t: torch.Tensor, device, dtypes=(torch.float32,)):
     if not t.is_cuda:
         raise RuntimeError(f"gfd GATConv: {name} must be on a HIP device (got {t.device})")
     if t.device != device:
         raise RuntimeError(f"gfd GATConv: {name} is on {t.device}, expected {device}")
-    if t.dtype != torch.float32:
-        raise TypeError(f"gfd GATConv: {name} must be float32 (got {t.dtype})")
+    if t.dtype not in dtypes:
+        raise TypeError(f"gfd GATConv: {name} must be {' or '.join(map(str, dtypes))} "
+                        f"(got {t.dtype})")
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    """x with unit feature stride (any row pitch is passed through as is)."""
+    return x if x.stride(1) == 1 and x.stride(0) >= x.size(1) else x.contiguous()
 
 
 class GATConvFunction(torch.autograd.Function):
@@ -43,11 +49,12 @@ class GATConvFunction(torch.autograd.Function):
     def forward(ctx, x, weight, att_src, att_dst, bias, graph: CSRGraph, negative_slope: float,
                 dropout_p: float, seed: int):
         dev = x.device
-        for n, t in (("x", x), ("weight", weight), ("att_src", att_src), ("att_dst", att_dst)):
+        _check_tensor("x", x, dev, (torch.float32, torch.bfloat16))
+        for n, t in (("weight", weight), ("att_src", att_src), ("att_dst", att_dst)):
             _check_tensor(n, t, dev)
         if bias is not None:
             _check_tensor("bias", bias, dev)
-        x = x.contiguous()
+        x = _rows(x)
         weight = weight.contiguous()
         att_src = att_src.contiguous()
         att_dst = att_dst.contiguous()
@@ -61,7 +68,8 @@ class GATConvFunction(torch.autograd.Function):
         stats = torch.empty((N, 2 * H), dtype=torch.float32, device=dev) if need_stats else None
         lib = _lib.load()
         ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, plan.num_hubs, plan.num_chunks), dev)
-        _lib.call("gfd_gat_fwd", x.data_ptr(), N, F, F, graph.rowptr.data_ptr(),
+        _lib.call("gfd_gat_fwd", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+                  graph.rowptr.data_ptr(),
                   graph.col.data_ptr(), weight.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(),
                   _lib.ptr(bias), H, C, float(negative_slope), float(dropout_p),
                   int(seed) & (2 ** 64 - 1), plan.cstruct(), out.data_ptr(), st.data_ptr(),
@@ -79,23 +87,29 @@ class GATConvFunction(torch.autograd.Function):
         slope, dp, seed, has_bias = ctx.meta
         dev = x.device
         g = grad_out.contiguous().to(torch.float32)
+        xin = x
+        if x.dtype != torch.float32:  # bf16 features: the backward reads fp32 rows
+            x = x.float()
         N, F = x.shape
         H, C = SUPPORTED_HEADS, weight.size(0) // SUPPORTED_HEADS
         csc = graph.csc()
-        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gx = torch.empty((N, F), dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
         gw = torch.empty_like(weight)
         gas = torch.empty_like(att_src)
         gad = torch.empty_like(att_dst)
         gb = torch.empty((C,), dtype=torch.float32, device=dev) if has_bias else None
         lib = _lib.load()
         ws = _ws(lib.gfd_gat_bwd_workspace_size(N, graph.num_messages, F, H, C), dev)
-        _lib.call("gfd_gat_bwd", x.data_ptr(), N, F, F, graph.rowptr.data_ptr(),
+        _lib.call("gfd_gat_bwd", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+                  graph.rowptr.data_ptr(),
                   graph.col.data_ptr(), csc.colptr.data_ptr(), csc.dst.data_ptr(),
                   csc.eid.data_ptr(), graph.num_messages, weight.data_ptr(), att_src.data_ptr(),
                   att_dst.data_ptr(), H, C, slope, dp, seed & (2 ** 64 - 1), st.data_ptr(),
                   stats.data_ptr(), g.data_ptr(), _lib.ptr(gx), gw.data_ptr(), gas.data_ptr(),
                   gad.data_ptr(), _lib.ptr(gb), ws.data_ptr(), ws.numel(),
                   _lib.stream_handle(dev))
+        if gx is not None and xin.dtype != torch.float32:
+            gx = gx.to(xin.dtype)
         return gx, gw, gas, gad, gb, None, None, None, None
 
 
@@ -124,7 +138,8 @@ class GATConv(nn.Module):
     """PyG-compatible ``GATConv`` for the reference's configuration.
 
     Supported: ``heads=8``, ``out_channels=64``, ``concat=False``,
-    ``add_self_loops=True``, any ``in_channels <= 256``, optional bias.
+    ``add_self_loops=True``, any ``in_channels <= 256``, optional bias; x in
+    float32 or bfloat16 (config C5: converted exactly on load, fp32 arithmetic).
     Anything else raises ``NotImplementedError`` rather than computing
     something different from PyG.
     """

@@ -17,10 +17,13 @@
  *  - The caller owns all memory, including workspaces; the library allocates
  *    nothing and keeps no global state.  All work is enqueued on ``stream``;
  *    nothing synchronises except where a function says so.
- *  - Floating point is IEEE fp32 at the boundary.  Internally the feature
- *    projection runs on f16 MFMA with a 3-term hi/lo split over power-of-two
- *    scaled rows (~2^-21 relative, fp32-faithful); logits are exact fp32 MFMA;
- *    softmax, aggregation and accumulation are fp32.
+ *  - Node features x are fp32 (GFD_DTYPE_F32, configs C1-C4) or bf16
+ *    (GFD_DTYPE_BF16, config C5), row-major with any row pitch; every other
+ *    floating-point argument is IEEE fp32.  Internally the feature projection
+ *    runs on f16 MFMA with a 3-term hi/lo split over power-of-two scaled rows
+ *    (~2^-21 relative, fp32-faithful); logits are exact fp32 MFMA; softmax,
+ *    aggregation and accumulation are fp32.  A bf16 x is converted exactly on
+ *    load, so the result is the fp32 forward of the bf16-rounded features.
  *  - Graph layout: ``edge_index`` is the reference's COO ``int64 [2, E]``
  *    (dataset.py:104; row 0 = source j, row 1 = destination i, flow
  *    source->target).  Internally a destination-sorted CSR of int32 with the
@@ -47,6 +50,10 @@ typedef int32_t gfd_status;
 #define GFD_ERR_HIP 4         /* a HIP runtime call or kernel launch failed                            */
 #define GFD_ERR_UNSUPPORTED 5 /* heads/channels/features outside the compiled set (H=8, C=64, F<=256)  */
 
+/* Element type of the node features x (``x_dtype`` arguments). */
+#define GFD_DTYPE_F32 0
+#define GFD_DTYPE_BF16 1
+
 const char* gfd_status_string(gfd_status status);
 int gfd_abi_version(void);
 
@@ -66,6 +73,13 @@ size_t gfd_csr_workspace_size(int64_t num_edges, int64_t num_nodes);
 gfd_status gfd_csr_from_coo(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
                             int32_t* rowptr, int32_t* col, void* ws, size_t ws_bytes,
                             gfd_stream_t stream);
+
+/* 128-bit fingerprint of a COO edge list (two independent position-sensitive
+ * 64-bit hashes of every (position, src, dst), device out[2]; no sync).  The
+ * graph cache keys on it so that a re-uploaded but equal edge_index (the
+ * reference's per-epoch batch.to(device), train.py:105) reuses its CSR. */
+gfd_status gfd_coo_fingerprint(const int64_t* edge_index, int64_t num_edges, uint64_t* out,
+                               gfd_stream_t stream);
 
 /* Source-sorted view of a CSR (for the backward scatter to sources):
  * colptr[N+1]; for the k-th message leaving source j (stable in CSR order),
@@ -99,10 +113,17 @@ gfd_status gfd_plan_order(const int32_t* rowptr, int64_t num_dst, int32_t cap, i
 /* Slot descriptors: desc[4*s .. 4*s+3] = {row, e_begin, e_end, hub_rank} of
  * tile slot s (row = order[s], or s when order is NULL; hub_rank -1 when
  * NULL) and, when slot_cols is not NULL, slot_cols[8*s + k] = col[min(e_begin
- * + k, e_end - 1)] (the first 8 sources, prefetched one tile ahead). */
+ * + k, e_end - 1)] (the first 8 sources, prefetched one tile ahead).
+ * class_split (nullable, device int64[2]) receives the slot class boundaries
+ * the forward's tile stage schedules by: class_split[0] = 1 + the last slot
+ * that is a hub or has more than 4 messages, class_split[1] = 1 + the last
+ * slot that is a hub or has more than 1 message (0 when there is none).
+ * Slots past class_split[0] are "light" (2..4 messages), slots past
+ * class_split[1] "lone" (self loop only).  Correct for ANY order: an order
+ * that is not degree-sorted only moves the boundaries towards num_dst. */
 gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t num_dst,
                          const int32_t* order, const int32_t* hub_rank, int32_t* desc,
-                         int32_t* slot_cols, gfd_stream_t stream);
+                         int32_t* slot_cols, int64_t* class_split, gfd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * GATConv forward (PyG GATConv.forward, concat=False, add_self_loops=True,
@@ -118,16 +139,18 @@ gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t num_
 /* Packed weights (device bytes): folded logit vectors and MFMA fragments. */
 size_t gfd_gat_packed_size(int in_features, int heads, int channels);
 
-/* lin_src.weight [H*C, F] row-major, att_src/att_dst [H*C] (PyG [1,H,C]) -> packed. */
+/* lin_src.weight [H*C, F] row-major, att_src/att_dst [H*C] (PyG [1,H,C]) -> packed
+ * (fp16 hi/lo fragments of W / H and of Wbar = mean_h W_h, folded logit
+ * vectors, power-of-two scales). */
 gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const float* att_dst,
                                 int in_features, int heads, int channels, void* packed,
                                 gfd_stream_t stream);
 
 /* Per-node attention logits st[r, 0:H] = s_r, st[r, H:2H] = t_r for rows
  * r in [0, num_rows) of x (x may point at any row; x_stride in elements). */
-gfd_status gfd_gat_logits(const float* x, int64_t num_rows, int in_features, int64_t x_stride,
-                          const void* packed, int heads, int channels, float* st,
-                          gfd_stream_t stream);
+gfd_status gfd_gat_logits(const void* x, int x_dtype, int64_t num_rows, int in_features,
+                          int64_t x_stride, const void* packed, int heads, int channels,
+                          float* st, gfd_stream_t stream);
 
 /* Execution plan of one destination range (all device pointers; NULL plan =
  * identity order, no hubs).  Built once per graph by gfd_plan_order and
@@ -140,6 +163,8 @@ typedef struct gfd_plan {
   const int32_t* hub_chunk;     /* [4*num_chunks] {hub, e_begin, e_end, dst}           */
   const int32_t* hub_chunk_ptr; /* [num_hubs + 1]                                      */
   const int32_t* hub_dst;       /* [num_hubs]                                          */
+  const int64_t* class_split;   /* [2] gfd_plan_desc class boundaries, or NULL: every  */
+                                /* slot runs the general tile kernel                   */
   int64_t num_hubs;
   int64_t num_chunks;
 } gfd_plan;
@@ -156,33 +181,44 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int in_fea
  * backward.  out [num_dst, C]; stats (nullable) [num_dst, 2H] = per-head
  * softmax max and denominator (sum of exp, without the eps) for the backward.
  * ``stages`` selects GFD_STAGE_HUBS (chunk partials + merge into ws),
- * GFD_STAGE_TILES (the fused tile kernel, reading merged hub rows from ws) or
- * GFD_STAGE_ALL; split calls must pass the same ws. */
+ * GFD_STAGE_TILES (the tile kernels of every destination class, reading the
+ * merged hub rows from ws) or GFD_STAGE_ALL; split calls must pass the same ws.
+ * The tile stage schedules destinations by the plan's classes: general (hub
+ * rows, 5+ messages), light (2..4), lone (self loop only). */
 #define GFD_STAGE_HUBS 1
 #define GFD_STAGE_TILES 2
 #define GFD_STAGE_ALL 3
-gfd_status gfd_gat_aggregate(const float* x, int64_t num_nodes, int in_features, int64_t x_stride,
-                             const int32_t* rowptr, const int32_t* col, int64_t num_dst,
-                             int64_t dst_offset, const float* st, const void* packed,
-                             const float* bias, int heads, int channels, float negative_slope,
-                             float dropout_p, uint64_t dropout_seed, const gfd_plan* plan,
-                             int stages, float* out, float* stats, void* ws, size_t ws_bytes,
-                             gfd_stream_t stream);
+/* single tile classes (profiling splits; the union equals GFD_STAGE_TILES):
+ * general (k_mid / k_fused), light (k_stream), lone (k_lone) */
+#define GFD_STAGE_TILES_GENERAL 4
+#define GFD_STAGE_TILES_LIGHT 8
+#define GFD_STAGE_TILES_LONE 16
+gfd_status gfd_gat_aggregate(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                             int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                             int64_t num_dst, int64_t dst_offset, const float* st,
+                             const void* packed, const float* bias, int heads, int channels,
+                             float negative_slope, float dropout_p, uint64_t dropout_seed,
+                             const gfd_plan* plan, int stages, float* out, float* stats, void* ws,
+                             size_t ws_bytes, gfd_stream_t stream);
 
 /* gfd_gat_logits plus max |x| over the given rows: xmax (nullable, one device
  * float) is combined with its current value by atomic max, so initialise it to
  * 0 and, for a row-sharded x, reduce it over the shards (max) before
  * gfd_gat_aggregate_ex.  Replaces the same PyG GATConv.forward step as
  * gfd_gat_logits. */
-gfd_status gfd_gat_logits_ex(const float* x, int64_t rows, int in_features, int64_t x_stride,
-                             const void* packed, int heads, int channels, float* st,
-                             float* xmax, gfd_stream_t stream);
+gfd_status gfd_gat_logits_ex(const void* x, int x_dtype, int64_t rows, int in_features,
+                             int64_t x_stride, const void* packed, int heads, int channels,
+                             float* st, float* xmax, gfd_stream_t stream);
 
 /* gfd_gat_aggregate with xmax (nullable) = max |x| over ALL rows of x.  Every
  * aggregated row is a convex combination of x rows (dropout: times 1/(1-p)),
  * so the tile stage then uses one power-of-two scale for every Z row instead
- * of a per-row max (same results within the operator's fp32 tolerance). */
-gfd_status gfd_gat_aggregate_ex(const float* x, int64_t num_nodes, int in_features,
+ * of a per-row max.  Precondition: *xmax >= max |x| over every row any
+ * destination gathers (the logits pass over all rows, reduced over shards).
+ * The single scale is taken only while max |x| <= 2^20; beyond that (heavy-
+ * tailed features, where small rows would lose the lo term) the kernels fall
+ * back to each row's own scale, so results stay within the fp32 tolerance. */
+gfd_status gfd_gat_aggregate_ex(const void* x, int x_dtype, int64_t num_nodes, int in_features,
                                 int64_t x_stride, const int32_t* rowptr, const int32_t* col,
                                 int64_t num_dst, int64_t dst_offset, const float* st,
                                 const float* xmax, const void* packed, const float* bias,
@@ -194,12 +230,12 @@ gfd_status gfd_gat_aggregate_ex(const float* x, int64_t num_nodes, int in_featur
 /* One-call GATConv forward over the whole graph (num_dst = N, offset 0):
  * pack weights + logits + aggregate.  st (nullable, [N, 2H]) receives the
  * logits; ws must hold gfd_gat_fwd_workspace_size(N, N, F, H, C, hubs, chunks). */
-gfd_status gfd_gat_fwd(const float* x, int64_t num_nodes, int in_features, int64_t x_stride,
-                       const int32_t* rowptr, const int32_t* col, const float* weight,
-                       const float* att_src, const float* att_dst, const float* bias, int heads,
-                       int channels, float negative_slope, float dropout_p, uint64_t dropout_seed,
-                       const gfd_plan* plan, float* out, float* st, float* stats, void* ws,
-                       size_t ws_bytes, gfd_stream_t stream);
+gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                       int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                       const float* weight, const float* att_src, const float* att_dst,
+                       const float* bias, int heads, int channels, float negative_slope,
+                       float dropout_p, uint64_t dropout_seed, const gfd_plan* plan, float* out,
+                       float* st, float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * GATConv backward (autograd of the PyG dataflow).
@@ -211,7 +247,8 @@ gfd_status gfd_gat_fwd(const float* x, int64_t num_nodes, int in_features, int64
 size_t gfd_gat_bwd_workspace_size(int64_t num_nodes, int64_t num_messages, int in_features,
                                   int heads, int channels);
 
-gfd_status gfd_gat_bwd(const float* x, int64_t num_nodes, int in_features, int64_t x_stride,
+gfd_status gfd_gat_bwd(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                       int64_t x_stride,
                        const int32_t* rowptr, const int32_t* col, const int32_t* colptr,
                        const int32_t* csc_dst, const int32_t* csc_eid, int64_t num_messages,
                        const float* weight, const float* att_src, const float* att_dst,

@@ -170,6 +170,48 @@ def gatconv_forward_at(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor,
     return agg.mean(dim=1) + bias
 
 
+class gatconv_forward_sampled:  # noqa: N801 (a namespace: prepare once, run many)
+    """PyG-dataflow outputs for a destination sample of a (device) CSR, with
+    only the rows the sample gathers copied to the host.  ``prepare`` builds
+    the induced sub-problem (the rows of every source of the sampled
+    destinations and of the destinations themselves, as fp32 on the CPU);
+    ``run`` is the same dataflow as ``gatconv_forward_at``.  Used by the
+    full-size parity tests (tests/test_bench_parity_gpu.py) and by bench.py's
+    CPU-baseline leg."""
+
+    @staticmethod
+    def prepare(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor,
+                dsts: torch.Tensor) -> dict:
+        dsts = dsts.long()
+        rp = rowptr.long()
+        starts, ends = rp[dsts], rp[dsts + 1]
+        lens = ends - starts
+        seg = torch.repeat_interleave(torch.arange(dsts.numel(), device=dsts.device), lens)
+        off = torch.cumsum(lens, 0) - lens
+        pos = starts[seg] + torch.arange(int(lens.sum()), device=dsts.device) - off[seg]
+        j = col[pos].long()
+        nodes, inv = torch.unique(torch.cat([j, dsts]), return_inverse=True)
+        return {"x": x[nodes].float().cpu(), "jl": inv[:j.numel()].cpu(),
+                "il": inv[j.numel():].cpu(), "seg": seg.cpu(), "n": dsts.numel(),
+                "rows": nodes.numel(), "dsts": dsts.cpu()}
+
+    @staticmethod
+    def run(sub: dict, weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor,
+            bias: Optional[torch.Tensor], heads: int = 8) -> torch.Tensor:
+        H = heads
+        C = weight.size(0) // H
+        h = (sub["x"] @ weight.t()).view(-1, H, C)
+        a_src = (h * att_src.reshape(1, H, C)).sum(-1)
+        a_dst = (h * att_dst.reshape(1, H, C)).sum(-1)
+        jl, il, seg, n = sub["jl"], sub["il"], sub["seg"], sub["n"]
+        logit = F.leaky_relu(a_src[jl] + a_dst[il][seg], NEG_SLOPE)
+        alpha = segment_softmax(logit, seg, n)
+        agg = torch.zeros((n, H, C), dtype=h.dtype).index_add(0, seg,
+                                                                alpha.unsqueeze(-1) * h[jl])
+        out = agg.mean(dim=1)
+        return out + bias if bias is not None else out
+
+
 def glorot_(t: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:
     """PyG ``inits.glorot``: U(-a, a), a = sqrt(6 / (fan_in + fan_out)) over the last two dims."""
     a = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))

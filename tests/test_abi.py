@@ -48,7 +48,7 @@ def test_ctypes_table_matches_header(lib):
 
 
 def test_version_and_status_strings(lib):
-    assert lib.gfd_abi_version() == 1
+    assert lib.gfd_abi_version() == 2
     assert b"range" in lib.gfd_status_string(2)
     assert lib.gfd_status_string(99) == b"unknown status"
 
@@ -67,12 +67,22 @@ def test_workspace_queries(lib):
 def test_argument_errors_without_launch(lib):
     # null pointers / bad shapes are rejected before anything touches a device
     assert lib.gfd_csr_from_coo(None, 10, 0, None, None, None, 0, None) == 1
-    assert lib.gfd_gat_fwd(None, 10, 166, 166, None, None, None, None, None, None, 8, 64,
-                           ctypes.c_float(0.2), ctypes.c_float(0.0), 0, None, None, None, None,
-                           0, 0, None, None, None, None, 0, None) == 1
-    assert lib.gfd_gat_fwd(None, 10, 166, 166, None, None, None, None, None, None, 4, 64,
-                           ctypes.c_float(0.2), ctypes.c_float(0.0), 0, None, None, None, None,
-                           0, 0, None, None, None, None, 0, None) == 5
+    # gfd_gat_fwd takes exactly the 23 parameters of include/gfd.h (ctypes checks the count)
+    args = [None, 0, 10, 166, 166, None, None, None, None, None, None, 8, 64, 0.2, 0.0, 0, None,
+            None, None, None, None, 0, None]
+    assert len(args) == len(lib.gfd_gat_fwd.argtypes) == 23
+    assert lib.gfd_gat_fwd(*args) == 1                       # null x
+    args[11] = 4
+    assert lib.gfd_gat_fwd(*args) == 5                       # heads != 8
+    x = ctypes.c_float(0.0)
+    args[11] = 8
+    args[0], args[1] = ctypes.addressof(x), 7                # unknown x_dtype
+    assert lib.gfd_gat_fwd(*args) == 1
+    # gfd_gat_bwd: bf16 features are not accepted by the backward (fp32 rows)
+    bargs = ([ctypes.addressof(x), 1, 1, 1, 1] + [None] * 5 + [1] + [None] * 3 +
+             [8, 64, 0.2, 0.0, 0] + [None] * 8 + [None, 0, None])
+    assert len(bargs) == len(lib.gfd_gat_bwd.argtypes)
+    assert lib.gfd_gat_bwd(*bargs) == 5
 
 
 def test_missing_library_fails_loudly(tmp_path):

@@ -1,0 +1,227 @@
+"""GPU parity at the benchmarked configurations and on the inputs that stress
+the tile stage's assumptions.
+
+* C4 exactly as bench.py builds and runs it (bench.setup + bench.Layer: 10M
+  nodes / 50M edges, F = 166 at row pitch 168 -- x is 6.7 GB, so rows above
+  4 GiB are gathered -- the max|x| single-scale path, the class-scheduled
+  tile stage): >= 512 sampled destinations (the 16 largest hubs, the 64
+  highest node ids, 64 slots of each class, random) against the oracle, and
+  the same through a 2-rank destination-sharded split.
+* C5's bf16 features (fp32 oracle on the bf16-rounded x).
+* Heavy-tailed features (max |x| = 1e6, 1e9), NaN-filled row padding with
+  the last row ending at the end of its allocation, plans whose slot order is
+  not degree-sorted, and the content-keyed graph cache.
+Oracle: oracle/gatconv_ref.py (gatconv_forward_sampled: PyG dataflow on the
+rows the sampled destinations gather).  Tolerance: 1e-4 + 1e-4 |ref|.
+"""
+import pytest
+import torch
+
+from _util import assert_close
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+H, C = 8, 64
+
+
+def _sample(layer, s, extra=()):
+    g = s["graph"]
+    plan = layer.plan
+    N = g.num_nodes
+    deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
+    light_b, lone_b = plan.classes()
+    order = plan.row_order.long()
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    pick = [torch.topk(deg, 16).indices,                              # largest hubs
+            torch.arange(N - 64, N, device=DEV)]                       # rows past 4 GiB of x
+    for lo, hi in ((0, light_b), (light_b, lone_b), (lone_b, N)):     # every class
+        if hi > lo:
+            pick.append(order[torch.randint(lo, hi, (64,), generator=gen, device=DEV)])
+    pick.append(torch.randint(0, N, (256,), generator=gen, device=DEV))
+    pick += [torch.as_tensor(e, device=DEV).long() for e in extra]
+    return torch.unique(torch.cat(pick))
+
+
+def _reference(s, dsts):
+    from oracle import gatconv_forward_sampled
+    sub = gatconv_forward_sampled.prepare(s["x"], s["graph"].rowptr, s["graph"].col, dsts)
+    return gatconv_forward_sampled.run(sub, s["W"].cpu(), s["a_s"].cpu(), s["a_d"].cpu(),
+                                       s["bias"].cpu())
+
+
+@pytest.fixture(scope="module")
+def c4():
+    import bench
+    s = bench.setup(DEV, 10_000_000, 50_000_000, 166)
+    s["bias"] = torch.randn(C, generator=torch.Generator().manual_seed(1)).to(DEV) * 0.1
+    yield s
+    del s
+    torch.cuda.empty_cache()
+
+
+def test_c4_bench_configuration_sampled_parity(c4):
+    import bench
+    s = c4
+    assert s["ldx"] == 168 and s["x"].stride(0) == 168
+    assert s["xbuf"].numel() * 4 > 2 ** 32                 # x is past 4 GiB
+    layer = bench.Layer(s, DEV, 1)
+    light_b, lone_b = layer.plan.classes()
+    assert 0 < light_b < lone_b < s["graph"].num_nodes     # all three classes present
+    assert layer.plan.num_hubs > 0
+    layer.step()
+    torch.cuda.synchronize()
+    out = layer.out
+    assert torch.isfinite(out).all()
+    dsts = _sample(layer, s)
+    assert dsts.numel() >= 512
+    assert_close(out[dsts], _reference(s, dsts), what="C4 bench config, sampled")
+
+
+def test_c4_two_rank_dst_shards(c4):
+    """The destination-sharded split (ranks 0 and 1 of 2, run one after the
+    other on this GPU) at the bench's size: each rank's shard plan, the
+    all-rows logits and max|x|, and the shard's outputs."""
+    import bench
+    from gfd import dist as gdist
+    s = dict(c4)
+    g = s["graph"]
+    outs = []
+    for r in range(2):
+        s["spec"] = gdist.ShardSpec(g.rowptr, r, 2)
+        s["shard"] = g.shard(s["spec"].dst_lo, s["spec"].dst_hi)
+        layer = bench.Layer(s, DEV, 1)      # world 1: logits over all rows = the all-gather
+        layer.step()
+        torch.cuda.synchronize()
+        outs.append((s["spec"], layer.out[:s["spec"].dst_hi - s["spec"].dst_lo].clone()))
+    out = torch.cat([o for _, o in outs])
+    assert out.shape[0] == g.num_nodes
+    lo1 = outs[1][0].dst_lo
+    edge = torch.arange(max(lo1 - 32, 0), min(lo1 + 32, g.num_nodes), device=DEV)
+    dsts = torch.unique(torch.cat([_sample(bench.Layer(c4, DEV, 1), c4), edge]))
+    assert_close(out[dsts], _reference(s, dsts), what="C4 2-rank shards, sampled")
+
+
+def _small(N, E, F, seed, dtype=torch.float32, pitch=None):
+    from gfd import synth
+    from oracle import glorot_
+    gen = torch.Generator().manual_seed(seed)
+    ei = torch.from_numpy(synth.power_law(N, E, seed=seed))
+    x = torch.randn(N, F, generator=gen)
+    W = glorot_(torch.empty(H * C, F), gen)
+    a_s = glorot_(torch.empty(1, H, C), gen)
+    a_d = glorot_(torch.empty(1, H, C), gen)
+    b = torch.randn(C, generator=gen) * 0.1
+    return ei, x, W, a_s, a_d, b
+
+
+def _gfd(x, ei, W, a_s, a_d, b, graph=None):
+    from gfd.nn import gat_conv
+    with torch.no_grad():
+        return gat_conv(x, graph if graph is not None else ei.to(DEV), W.to(DEV), a_s.to(DEV),
+                        a_d.to(DEV), b.to(DEV))
+
+
+def _oracle(x, ei, W, a_s, a_d, b):
+    from oracle import gatconv_forward
+    with torch.no_grad():
+        return gatconv_forward(x, ei, W, a_s, a_d, b)
+
+
+@pytest.mark.parametrize("F", [64, 128, 166])
+def test_bf16_features_match_fp32_oracle_on_rounded_x(F):
+    ei, x, W, a_s, a_d, b = _small(30000, 240000, F, seed=11)
+    xb = x.to(torch.bfloat16)
+    out = _gfd(xb.to(DEV), ei, W, a_s, a_d, b)
+    assert out.dtype == torch.float32
+    assert_close(out, _oracle(xb.float(), ei, W, a_s, a_d, b), what=f"bf16 x, F={F}")
+
+
+def test_c5_shape_bf16_sampled_parity():
+    """The C5 generator and layout (bf16, row pitch 168) at 2M / 20M."""
+    import bench
+    s = bench.setup(DEV, 2_000_000, 20_000_000, 166, dtype=torch.bfloat16)
+    s["bias"] = torch.randn(C, generator=torch.Generator().manual_seed(2)).to(DEV) * 0.1
+    assert s["ldx"] == 168 and s["x"].dtype == torch.bfloat16
+    layer = bench.Layer(s, DEV, 1)
+    layer.step()
+    torch.cuda.synchronize()
+    dsts = _sample(layer, s)
+    assert_close(layer.out[dsts], _reference(s, dsts), what="C5-shaped bf16, sampled")
+
+
+@pytest.mark.parametrize("big", [1e6, 1e9])
+def test_heavy_tailed_features(big):
+    """One outlier feature: the single Z-row scale would push every other row
+    into fp16 subnormals; the kernels fall back to per-row scales."""
+    ei, x, W, a_s, a_d, b = _small(6000, 48000, 166, seed=12)
+    x[0, 0] = big
+    x[1, 5] = -big / 3
+    out = _gfd(x.to(DEV), ei, W, a_s, a_d, b)
+    assert_close(out, _oracle(x, ei, W, a_s, a_d, b), what=f"outlier {big:g}")
+
+
+@pytest.mark.parametrize("big", [1e6, 1e9])
+def test_heavy_tailed_features_sharded(big):
+    from gfd import dist as gdist, graph as ggraph
+    ei, x, W, a_s, a_d, b = _small(6000, 48000, 166, seed=13)
+    x[3, 7] = big
+    xd, Wd, asd, add, bd = x.to(DEV), W.to(DEV), a_s.to(DEV), a_d.to(DEV), b.to(DEV)
+    g = ggraph.csr_from_coo(ei.to(DEV), 6000)
+    packed = gdist.pack_weights(Wd, asd, add)
+    parts = []
+    xmax = torch.zeros(1, device=DEV)
+    specs = [gdist.ShardSpec(g.rowptr, r, 2) for r in range(2)]
+    st = torch.cat([gdist.shard_logits(xd, packed, sp, xmax) for sp in specs])
+    for sp in specs:
+        parts.append(gdist.shard_aggregate(xd, g, st, packed, bd, sp, xmax=xmax))
+    torch.cuda.synchronize()
+    assert_close(torch.cat(parts), _oracle(x, ei, W, a_s, a_d, b), what=f"sharded outlier {big:g}")
+
+
+@pytest.mark.parametrize("F", [100, 166])
+def test_nan_row_padding_and_last_row_at_allocation_end(F):
+    """x with row pitch > F whose padding columns hold NaN, and whose last row
+    ends exactly at the end of the allocation: lanes f >= F must read zeros
+    (buffer range check), never the padding or past the allocation."""
+    N = 5000
+    ei, x, W, a_s, a_d, b = _small(N, 40000, F, seed=14)
+    ldx = (F + 7) // 8 * 8 + 8
+    buf = torch.full((N * ldx - (ldx - F),), float("nan"), device=DEV)
+    xv = buf.as_strided((N, F), (ldx, 1))
+    xv.copy_(x.to(DEV))
+    assert torch.isnan(buf.as_strided((N - 1, ldx - F), (ldx, 1), F)).all()
+    out = _gfd(xv, ei, W, a_s, a_d, b)
+    assert torch.isfinite(out).all()
+    assert_close(out, _oracle(x, ei, W, a_s, a_d, b), what=f"NaN padding F={F}")
+
+
+@pytest.mark.parametrize("order,cap", [(False, None), (True, 2), (True, 4)])
+def test_plan_orders_that_are_not_degree_sorted(order, cap):
+    """Class boundaries are exact for any slot order: no order at all, and an
+    order whose degree cap merges light and general rows."""
+    from gfd import graph as ggraph
+    ei, x, W, a_s, a_d, b = _small(20000, 160000, 166, seed=15)
+    g = ggraph.csr_from_coo(ei.to(DEV), 20000)
+    g._plan = ggraph.build_plan(g.rowptr, g.num_messages, order=order, col=g.col, order_cap=cap)
+    out = _gfd(x.to(DEV), ei, W, a_s, a_d, b, graph=g)
+    assert_close(out, _oracle(x, ei, W, a_s, a_d, b), what=f"order={order} cap={cap}")
+
+
+def test_graph_cache_hits_equal_edge_index_in_new_tensor():
+    """The reference's loop re-uploads the graph every epoch (train.py:105):
+    an equal edge_index in a new tensor must reuse the CSR (and its plan)."""
+    from gfd import graph as ggraph
+    ggraph.clear_cache()
+    ei = torch.randint(0, 1000, (2, 5000))
+    g1 = ggraph.get_graph(ei.to(DEV), 1000)
+    g1.plan()
+    g2 = ggraph.get_graph(ei.clone().to(DEV), 1000)
+    assert g2 is g1 and g2._plan is not None
+    ei2 = ei.clone()
+    ei2[0, 17] = (ei2[0, 17] + 1) % 1000
+    g3 = ggraph.get_graph(ei2.to(DEV), 1000)
+    assert g3 is not g1
+    e3 = ei.to(DEV)
+    g4 = ggraph.get_graph(e3, 1000)
+    e3[1, 0] = (e3[1, 0] + 1) % 1000          # in-place edit: version counter moves
+    assert ggraph.get_graph(e3, 1000) is not g4

@@ -128,13 +128,17 @@ def test_backward_vs_oracle_elliptic_like():
 
 
 @pytest.mark.parametrize("threshold,chunk", [(1, 1), (4, 3), (16, 16), (1 << 30, 128)])
-def test_hub_split_equivalence(threshold, chunk):
-    """Same outputs whatever the hub threshold/chunking (merge is exact math)."""
+@pytest.mark.parametrize("classes", [False, True])
+def test_hub_split_equivalence(threshold, chunk, classes):
+    """Same outputs whatever the hub threshold/chunking (merge is exact math),
+    through k_fused (plan without slot sources) and through the
+    class-scheduled kernels (k_mid / k_stream / k_lone)."""
     gnn, graph = _gfd()
     x, ei, conv = _random_case(800, 6000, 166, seed=4)
     xd, eid = x.to(DEV), ei.to(DEV)
     g = graph.csr_from_coo(eid, 800)
-    g._plan = graph.build_plan(g.rowptr, g.num_messages, threshold=threshold, chunk=chunk)
+    g._plan = graph.build_plan(g.rowptr, g.num_messages, threshold=threshold, chunk=chunk,
+                               col=g.col if classes else None)
     with torch.no_grad():
         out = gnn.gat_conv(xd, g, conv.lin_src.weight.to(DEV), conv.att_src.to(DEV),
                            conv.att_dst.to(DEV), conv.bias.to(DEV))
