@@ -6,8 +6,8 @@
 //   out_i = sum_h W_h z_ih / H + bias   (MFMA over K = 8 * Fp)
 // Destinations are scheduled by class (the plan's descending-degree slot order):
 //   hubs  (> threshold messages)   k_hub_partial / k_hub_fin   (gfd_hub.hip)
-//   general (hub rows, 5+ msgs)    k_mid    16 waves, W from L2 (gfd_mid.hip)
-//   light (2..4 messages)          k_stream 8 waves, W stationary (gfd_stream.hip)
+//   general (hub rows, 5+ msgs)    k_stream<LIGHT = false>  8 waves, W stationary
+//   light (2..4 messages)          k_stream<LIGHT = true>   (gfd_stream.hip)
 //   lone  (self loop only)         k_lone   out = mean_h W_h x_i  (gfd_lone.hip)
 //   F > 168 / no plan              k_fused  (gfd_fused.hip)
 #pragma once
@@ -200,7 +200,11 @@ __device__ __forceinline__ int pack_zrow(const f32x2 (&z)[4][KF], float inv, int
 #pragma unroll
   for (int g = 0; g < 4; ++g) i2[g] = bcast2(inv, 2 * g);
   int er = erg;
+#ifdef GFD_AB_GS_ONLY
+  if (false) {
+#else
   if (erg == 127) {
+#endif
     float zm = 0.f;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -352,7 +356,7 @@ bool ensure_lds(const void* kernel, size_t bytes);
 
 gfd_status launch_hubs(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 // tile stages; GFD_ERR_UNSUPPORTED when the configuration is outside the kernel's set
-gfd_status launch_mid(const AggArgs& a, const PackLayout& L, hipStream_t stream);
+gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end, hipStream_t stream);
 gfd_status launch_lone(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_fused(const AggArgs& a, const PackLayout& L, hipStream_t stream);

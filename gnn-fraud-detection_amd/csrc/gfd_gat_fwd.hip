@@ -4,8 +4,8 @@
 //
 //   stage HUBS   k_hub_partial + k_hub_fin (gfd_hub.hip)
 //   stage TILES  with a slot plan and F <= 168:
-//                  general slots  k_mid     (gfd_mid.hip)
-//                  light slots    k_stream  (gfd_stream.hip)
+//                  general slots  k_stream<LIGHT = false>  (gfd_stream.hip)
+//                  light slots    k_stream<LIGHT = true>
 //                  lone slots     k_lone    (gfd_lone.hip)
 //                otherwise        k_fused   (gfd_fused.hip)
 // Classes come from the plan's class_split (gfd_plan_desc); with dropout, or
@@ -77,11 +77,11 @@ gfd_status tiles_impl(const AggArgs& a, const PackLayout& L, hipStream_t stream)
                          a.slope >= 0.f && a.slope <= 1.f;
   if (!plan_path) return (cls & kMidBit) ? launch_fused(a, L, stream) : GFD_OK;
   if (cls & kMidBit) {
-    const gfd_status s = launch_mid(a, L, stream);
+    const gfd_status s = launch_general(a, L, stream);
     if (s == GFD_ERR_UNSUPPORTED) return launch_fused(a, L, stream);
     if (s != GFD_OK) return s;
   }
-  if (!p.class_split || a.dp > 0.f) return GFD_OK;  // k_mid took every tile
+  if (!p.class_split || a.dp > 0.f) return GFD_OK;  // the general kernel took every tile
   // lone slots need 16-B aligned rows; otherwise the light kernel runs to the end
   const uintptr_t base = reinterpret_cast<uintptr_t>(a.x);
   const int eb = a.xdt == GFD_DTYPE_BF16 ? 2 : 4;

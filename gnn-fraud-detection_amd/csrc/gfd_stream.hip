@@ -1,6 +1,7 @@
-// gfd_stream.hip -- light destinations (2..4 messages incl. the self loop):
-// the PyG GATConv.forward softmax-aggregate-project of
-// /root/reference/src/models/gat.py:80 for the bulk of a power-law graph.
+// gfd_stream.hip -- general (hub rows and 5+ messages) and light (2..4
+// messages incl. the self loop) destinations: the PyG GATConv.forward
+// softmax-aggregate-project of /root/reference/src/models/gat.py:80 for the
+// bulk of a power-law graph.  One kernel template, two instances (LIGHT).
 //
 // Weight-stationary streaming tile kernel (persistent, one 8-wave block per
 // CU, two waves per SIMD at up to 256 VGPRs):
@@ -11,15 +12,21 @@
 //  * Z goes through LDS once per 16-row tile in the feature-major K order
 //    p = 8 f + h, so a lane stores all 8 heads of its feature with one 16-B
 //    write per (hi, lo).  acc += Zhi.Whi + Zhi.Wlo + Zlo.Whi (lo unscaled).
-//  * Two destinations per wave (rows 2w, 2w+1).  All (at most 4) x rows of a
-//    slot are issued one tile ahead, between the MFMA k-steps of the current
-//    tile; records are loaded two tiles ahead.
+//  * Two destinations per wave (rows 2w, 2w+1).  The first 4 x rows of a slot
+//    (all of a light slot's) are issued one tile ahead, between the MFMA
+//    k-steps of the current tile; records are loaded two tiles ahead.
+//  * General slots (LIGHT = false) continue with an online softmax over
+//    batches of 8 messages: the sources of messages 8..71 come with the
+//    record (one 64-wide window of the CSR columns), so the logits and all 8
+//    rows of the next batch are issued together at the end of the current one
+//    (one memory round trip per batch); hub rows load their merged z.
 //  * Per tile: MFMA -> kh = 1 partials to LDS -> barrier -> kh = 0 waves reduce
 //    and store out (during the next tile's MFMA); every wave aggregates its
 //    next rows into Z -> barrier.
 //
 // LDS ownership (the invariant every access below keeps):
-//  * ring[par][r] (slot records) is private to the wave that owns slot r
+//  * ring[par][r] (slot records: descriptor and, general only, the first 8
+//    sources) is private to the wave that owns slot r
 //    (r = 2w, 2w + 1): written by that wave when it issues tile v + 1 (during
 //    MFMA(v), parity (v + 1) & 1) and read by the same wave after barrier 1 of
 //    iteration v.  The next write of that parity happens at iteration v + 2,
@@ -48,10 +55,16 @@ struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm 
   bool live;      // slot < num_dst (otherwise v is a clamped copy, row taken as -1)
 };
 
+struct SlotRing {  // a slot record parked in LDS between issue and aggregation
+  int4 d;          // {row (-1: empty), e_begin, e_end, hub_rank}
+  int j[8];        // sources of messages 0..7 (general slots)
+};
+
 template <int KF>
 struct SlotRows {  // a slot's first (and, for light slots, only) batch in flight
   float th;        // t_i of head lane & 7
   float sj;        // s_j of the lane's message (lane >> 3)
+  int cj;          // general: source of message 8 + lane (0 past the end)
   float xv[4][KF];  // x rows of messages 0..3 (lane <-> feature)
 };
 
@@ -65,14 +78,16 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
   p.live = slot < num_dst;
 }
 
-// One piece of the issue of a slot: part 0 = logits (t_i, s_j) and the ring
-// record; part 1 + k = x row k.  Issued unconditionally (past the last slot:
-// clamped, ignored records), so no branch joins in-flight loads.
-template <int PART, typename XT, int KF>
+// One piece of the issue of a slot: part 0 = logits (t_i, s_j), the source
+// window (general) and the ring record; part 1 + k = x row k.  Issued
+// unconditionally (past the last slot: clamped, ignored records), so no
+// branch joins in-flight loads.
+template <int PART, typename XT, int KF, bool LIGHT>
 __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF>& q,
                                               const void* __restrict__ x, int64_t ldx, int F,
+                                              const int32_t* __restrict__ col,
                                               const float* __restrict__ st, int64_t dst_offset,
-                                              int4* __restrict__ ring, int lane) {
+                                              SlotRing* __restrict__ ring, int lane) {
   if constexpr (PART == 0) {
     const int h = lane & 7;
     const int row = __builtin_amdgcn_readlane(p.v, 0);  // >= 0: clamped slots are real rows
@@ -82,7 +97,16 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF>& q,
     const int jm = __builtin_amdgcn_ds_bpermute((8 + (lane >> 3)) << 2, p.v);  // message lane >> 3
     q.th = st[(dst_offset + row) * 16 + H + h];
     q.sj = st[int64_t(jm) * 16 + h];
-    if (lane == 0) *ring = make_int4(p.live ? row : -1, e0, e1, hw);
+    if constexpr (!LIGHT) {
+      // sources of messages 8 .. 71 (one per lane), range-checked: light, hub
+      // and empty slots fetch nothing
+      const int nx = (p.live && hw < 0 && e1 - e0 > 8) ? e1 - e0 - 8 : 0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int32_t*>(col) + e0 + 8, 0, nx * 4, 0x00020000);
+      q.cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+      if ((lane & 56) == 8) ring->j[lane & 7] = p.v;
+    }
+    if (lane == 0) ring->d = make_int4(p.live ? row : -1, e0, e1, hw);
   } else {
     constexpr int k = PART - 1;
     const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
@@ -149,21 +173,151 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF>& q, in
   }
 }
 
-template <typename XT, int KF, int KHM, int LO, bool EXACT>
+// A general slot (record in the ring, first 4 rows in q): un-normalised z
+// (head pairs, lane <-> feature) by an online softmax over batches of 8
+// messages, then normalised, scaled, split and written into the Z tile.
+//  * batch 0: logits and rows 0..3 were issued one tile ahead; rows 4..7 are
+//    issued on entry.
+//  * batches 1..: sources come from the cj window (lane i = message cb + i),
+//    so the logits and all 8 rows of the next batch are issued together at
+//    the end of the current one (one memory round trip per batch; a col ->
+//    st -> rows chain would be three).
+//  * hub rows: the merged, normalised z of k_hub_fin.
+template <typename XT, int KF>
+__device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
+                                           const SlotRows<KF>& q, const void* __restrict__ x,
+                                           int64_t ldx, int F, int Fp,
+                                           const int32_t* __restrict__ col,
+                                           const float* __restrict__ st, float slope, float dp,
+                                           uint64_t seed, const float* __restrict__ zhub,
+                                           float* __restrict__ stats, _Float16* __restrict__ zh,
+                                           _Float16* __restrict__ zl, float* __restrict__ rsc,
+                                           int* __restrict__ rid, int r, int erg, int lane) {
+  const int4 d = uni4(ring->d);
+  const int j0 = ring->j[lane >> 3];
+  const int h = lane & 7, kk = lane >> 3;
+  f32x2 z[4][KF];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
+  float inv = 1.0f;
+  if (d.x >= 0 && d.w >= 0) {  // hub: merged row (already normalised)
+    const float* src = zhub + int64_t(d.w) * (H * Fp);
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq) {
+        const int f = lane + 64 * qq;
+        if (f < Fp) z[g][qq] = f32x2{src[2 * g * Fp + f], src[(2 * g + 1) * Fp + f]};
+      }
+  } else if (d.x >= 0) {
+    const int e0 = d.y, e1 = d.z;
+    const int n = e1 - e0;
+    float xa[4][KF], xb[4][KF];
+    const float keep = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+    float m, l;
+    {  // batch 0
+      const bool valid = kk < n;
+      const float v = leaky01(q.sj + q.th, slope);
+      m = max_xor8_16_32(valid ? v : -INFINITY);
+      float pv = valid ? __expf(v - m) : 0.f;
+      l = pv;
+      if (dp > 0.f) pv = dropout_keep(seed, uint32_t(e0 + kk), uint32_t(h), dp) ? pv * keep : 0.f;
+      fma_rows<KF, 4>(z, q.xv, pv, 0, min(4, n));
+      if (n > 4) {  // rows 4..7
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), ldx), F, lane,
+                           4 + k < n, xb[k]);
+        fma_rows<KF, 4>(z, xb, pv, 4, min(4, n - 4));
+      }
+    }
+    // batches 1..: loads of batch b issued at the end of batch b - 8
+    int cj = q.cj, cb = 8;  // cj window: lane i = message cb + i
+    float sv = 0.f;
+    auto issue = [&](int b) {
+      if (b - cb >= 64) {  // past the window (more than 72 messages): next 64 sources
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int32_t*>(col) + e0 + b, 0, (n - b) * 4, 0x00020000);
+        cj = int(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+        cb = b;
+      }
+      const int jl = __builtin_amdgcn_ds_bpermute((b - cb + kk) << 2, cj);
+      sv = st[int64_t(jl) * 16 + h];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(cj, b - cb + k), ldx), F, lane,
+                         b + k < n, xa[k]);
+      if (n - b > 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(cj, b - cb + 4 + k), ldx), F,
+                           lane, b + 4 + k < n, xb[k]);
+      }
+    };
+    if (n > 8) issue(8);
+    for (int b = 8; b < n; b += 8) {
+      const bool valid = b + kk < n;
+      const float v = leaky01(sv + q.th, slope);
+      const float mn = fmaxf(m, max_xor8_16_32(valid ? v : -INFINITY));
+      const float sc = __expf(m - mn);
+      float pv = valid ? __expf(v - mn) : 0.f;
+      l = fmaf(l, sc, pv);
+      {  // rescale (unconditional: a wave-uniform branch here costs the register
+         // allocator more than the 12 multiplies it would skip)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x2 s2 = bcast2(sc, 2 * g);
+#pragma unroll
+          for (int qq = 0; qq < KF; ++qq) z[g][qq] *= s2;
+        }
+      }
+      m = mn;
+      if (dp > 0.f)
+        pv = dropout_keep(seed, uint32_t(e0 + b + kk), uint32_t(h), dp) ? pv * keep : 0.f;
+      fma_rows<KF, 4>(z, xa, pv, 0, min(4, n - b));
+      if (n - b > 4) fma_rows<KF, 4>(z, xb, pv, 4, min(4, n - b - 4));
+      if (b + 8 < n) issue(b + 8);
+    }
+    l = sum_xor8_16_32(l);
+    if (__builtin_expect(stats != nullptr, 0) && lane < 8) {  // training only
+      float* sr = stats + int64_t(d.x) * 16 + lane;
+      sr[0] = m;
+      sr[8] = l;
+    }
+    inv = __builtin_amdgcn_rcpf(l + kSoftmaxEps);
+  }
+  if (d.x < 0) {
+    if (lane == 0) rid[r] = -1;
+    return;
+  }
+  f16x8 hi[KF], lo[KF];
+  const int er = pack_zrow<KF>(z, inv, erg, hi, lo);
+  write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
+  if (lane == 0) {
+    rsc[r] = ldexpf(1.0f, -er);
+    rid[r] = d.x;
+  }
+}
+
+template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
-    const void* __restrict__ x, int F, int Fp, int64_t ldx, int64_t num_dst, int64_t dst_offset,
-    const int4* __restrict__ desc, const int32_t* __restrict__ cols8,
-    const float* __restrict__ st, const PackHeader* __restrict__ hdr,
-    const uint4* __restrict__ wsh, const uint4* __restrict__ wsl, const float* __restrict__ bias,
-    float slope, float* __restrict__ out, float* __restrict__ stats,
-    const float* __restrict__ xmax, const int64_t* __restrict__ split, int to_end) {
+    const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
+    int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
+    const int32_t* __restrict__ cols8, const float* __restrict__ st,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
+    const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
+    uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
+    float* __restrict__ stats, const float* __restrict__ xmax,
+    const int64_t* __restrict__ split, int to_end) {
   extern __shared__ __attribute__((aligned(16))) char ssm[];
   const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
   const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
   _Float16* Zh = reinterpret_cast<_Float16*>(ssm);              // [16][ZS]
   _Float16* Zl = Zh + kTile * ZS;                               // [16][ZS]
   f32x4* red0 = reinterpret_cast<f32x4*>(Zl + kTile * ZS);      // [2 parity][4 ct][64]
-  int4* ring0 = reinterpret_cast<int4*>(red0 + 2 * 4 * 64);     // [2 parity][16]
+  SlotRing* ring0 = reinterpret_cast<SlotRing*>(red0 + 2 * 4 * 64);  // [2 parity][16]
   float* rsc0 = reinterpret_cast<float*>(ring0 + 2 * kTile);    // [2][16] by tile parity
   int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);         // [2][16]
   uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);       // [8 waves][LO][64]
@@ -173,10 +327,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   const int r0 = 2 * wave, r1 = r0 + 1;
   const int64_t G = gridDim.x;
   const int64_t t0 = blockIdx.x;
+  // general tiles: [0, ceil(split[0] / 16)), every tile without a split;
   // light tiles: [ceil(split[0] / 16), ceil(split[1] / 16)) (to_end: up to the
-  // last tile, when k_lone does not run), tiles t0 + v G
-  const int64_t tb = (split[0] + kTile - 1) / kTile;
-  const int64_t te = ((to_end ? num_dst : split[1]) + kTile - 1) / kTile;
+  // last tile, when k_lone does not run); this block takes tiles t0 + v G
+  const int64_t all = (num_dst + kTile - 1) / kTile;
+  const int64_t tb = LIGHT ? (split[0] + kTile - 1) / kTile : 0;
+  const int64_t te = LIGHT ? ((to_end ? num_dst : split[1]) + kTile - 1) / kTile
+                           : (split ? (split[0] + kTile - 1) / kTile : all);
   const int64_t nv = t0 < te - tb ? (te - tb - 1 - t0) / G + 1 : 0;
   int lane = opaque(threadIdx.x & 63);
   auto slot = [&](int64_t v, int r) { return (tb + t0 + v * G) * kTile + r; };
@@ -185,7 +342,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   // after the first rows are issued
   const float bcol = bias ? bias[ct * 16 + (lane & 15)] : 0.f;
   const float wu = hdr->w_unscale;
-  const int erg = global_scale_exp(xmax, 0.f);
+  const int erg = global_scale_exp(xmax, dp);
   constexpr int NR = KHM - LO;  // k-steps (of KHM) with W_lo in registers
   f16x8 bh[KHM], bl[NR > 0 ? NR : 1];
 #pragma unroll
@@ -208,7 +365,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   sl_rec(n0, slot(0, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(0, r1), num_dst, desc, cols8, lane);
 #define GFD_ISSUE(P, n, d, ring) \
-  sl_issue_part<P, XT, KF>(n, d, x, ldx, F, st, dst_offset, ring, lane)
+  sl_issue_part<P, XT, KF, LIGHT>(n, d, x, ldx, F, col, st, dst_offset, ring, lane)
   GFD_ISSUE(0, n0, d0, ring0 + r0); GFD_ISSUE(1, n0, d0, ring0 + r0);
   GFD_ISSUE(2, n0, d0, ring0 + r0); GFD_ISSUE(3, n0, d0, ring0 + r0);
   GFD_ISSUE(4, n0, d0, ring0 + r0);
@@ -217,14 +374,25 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   GFD_ISSUE(4, n1, d1, ring0 + r1);
   sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
-  {
-    const int4 da = uni4(ring0[r0]), db = uni4(ring0[r1]);
-    const int kmax = max(da.z - da.y, db.z - db.y);
-    sl_light<KF>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0, rid0, r0, erg,
-                 lane);
-    sl_light<KF>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0, rid0, r1, erg,
-                 lane);
-  }
+  auto aggregate = [&](int tpar) {  // this wave's two slots of the tile in parity tpar
+    SlotRing* rg = ring0 + tpar * kTile;
+    float* rsc = rsc0 + tpar * kTile;
+    int* rid = rid0 + tpar * kTile;
+    if constexpr (LIGHT) {
+      const int4 da = uni4(rg[r0].d), db = uni4(rg[r1].d);
+      const int kmax = max(da.z - da.y, db.z - db.y);  // wave-uniform
+      sl_light<KF>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg,
+                   lane);
+      sl_light<KF>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg,
+                   lane);
+    } else {
+      sl_general<XT, KF>(rg + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                         Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane);
+      sl_general<XT, KF>(rg + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+                         Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg, lane);
+    }
+  };
+  aggregate(0);
   __syncthreads();
 
   // out rows of a finished tile (waves kh = 0): own K-half partial + the other
@@ -270,7 +438,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       // the next tile's rows are issued between the k-steps (the vector memory
       // pipe is idle in this phase): 10 pieces (per slot: header, 4 rows)
       // spread evenly, piece i in k-step i * KHM / 10
-      int4* rg = ring0 + pn * kTile;
+      SlotRing* rg = ring0 + pn * kTile;
 #define GFD_PIECE(i) (u == (i) * KHM / 10)
       if (GFD_PIECE(0)) GFD_ISSUE(0, n0, d0, rg + r0);
       if (GFD_PIECE(1)) GFD_ISSUE(1, n0, d0, rg + r0);
@@ -314,14 +482,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     __syncthreads();  // partials visible; every Z read of this tile done
 
     // ---- tile v + 1: aggregate its rows into Z ----
-    if (more) {
-      const int4 da = uni4(ring0[pn * kTile + r0]), db = uni4(ring0[pn * kTile + r1]);
-      const int kmax = max(da.z - da.y, db.z - db.y);  // wave-uniform
-      sl_light<KF>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc0 + pn * kTile,
-                   rid0 + pn * kTile, r0, erg, lane);
-      sl_light<KF>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc0 + pn * kTile,
-                   rid0 + pn * kTile, r1, erg, lane);
-    }
+    if (more) aggregate(pn);
     __syncthreads();  // Z of the next tile complete
   }
 #undef GFD_ISSUE
@@ -330,14 +491,14 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 
 size_t stream_smem(int Fp, int lo) {
   return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 2 * 4 * 64 +
-         sizeof(int4) * 2 * kTile + sizeof(float) * 4 * kTile +
+         sizeof(SlotRing) * 2 * kTile + sizeof(float) * 4 * kTile +
          sizeof(uint4) * kSWaves * lo * 64;
 }
 
-template <typename XT, int KF, int KHM, int LO, bool EXACT>
+template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
-  auto kern = &k_stream<XT, KF, KHM, LO, EXACT>;
+  auto kern = &k_stream<XT, KF, KHM, LO, EXACT, LIGHT>;
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
   const size_t lds = stream_smem(L.Fp, LO);
   if (L.KS / 2 > KHM || lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;
@@ -346,12 +507,15 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
   int64_t grid = cu_count();
   if (grid > tiles) grid = tiles;
   const gfd_plan& p = a.plan;
+  // general: with dropout (no light / lone classes) or no class split, every tile
+  const int64_t* split = (!LIGHT && a.dp > 0.f) ? nullptr : p.class_split;
   kern<<<int(grid), kSWaves * 64, lds, stream>>>(
-      a.x, a.F, L.Fp, a.ldx, a.num_dst, a.dst_offset, reinterpret_cast<const int4*>(p.slot_desc),
-      p.slot_cols, a.st, reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
+      a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
+      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
+      reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
-      reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.out, a.stats,
-      a.xmax, p.class_split, to_end ? 1 : 0);
+      reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
+      a.zhub, a.out, a.stats, a.xmax, split, to_end ? 1 : 0);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
@@ -359,18 +523,18 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
 // Instance for this K: KH = KS / 2 k-steps per wave, at most KHM = 8 / 16 / 21
 // for one / two / three feature chunks (F <= 64 / 128 / 168).  KF = 3 keeps
 // W_lo of 8 k-steps per wave in LDS.
-template <typename XT>
+template <typename XT, bool LIGHT>
 gfd_status launch_stream_x(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
   const int KF = kf_for(a.F);
   const bool exact = L.KS / 2 == (KF == 1 ? 8 : KF == 2 ? 16 : 21);
   switch (KF) {
-    case 1: return exact ? launch_stream_k<XT, 1, 8, 0, true>(a, L, to_end, stream)
-                         : launch_stream_k<XT, 1, 8, 0, false>(a, L, to_end, stream);
-    case 2: return exact ? launch_stream_k<XT, 2, 16, 0, true>(a, L, to_end, stream)
-                         : launch_stream_k<XT, 2, 16, 0, false>(a, L, to_end, stream);
-    case 3: return exact ? launch_stream_k<XT, 3, 21, 8, true>(a, L, to_end, stream)
-                         : launch_stream_k<XT, 3, 21, 8, false>(a, L, to_end, stream);
+    case 1: return exact ? launch_stream_k<XT, 1, 8, 0, true, LIGHT>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 1, 8, 0, false, LIGHT>(a, L, to_end, stream);
+    case 2: return exact ? launch_stream_k<XT, 2, 16, 0, true, LIGHT>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 2, 16, 0, false, LIGHT>(a, L, to_end, stream);
+    case 3: return exact ? launch_stream_k<XT, 3, 21, 8, true, LIGHT>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 3, 21, 8, false, LIGHT>(a, L, to_end, stream);
     default: return GFD_ERR_UNSUPPORTED;
   }
 }
@@ -380,13 +544,21 @@ gfd_status launch_stream_x(const AggArgs& a, const PackLayout& L, bool to_end,
 namespace gfd {
 namespace fwd {
 
+gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
+  const gfd_plan& p = a.plan;
+  if (!p.slot_desc || !p.slot_cols) return GFD_ERR_UNSUPPORTED;
+  if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
+  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, false>(a, L, false, stream)
+                                 : launch_stream_x<XF32, false>(a, L, false, stream);
+}
+
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
                         hipStream_t stream) {
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols || !p.class_split || a.dp > 0.f) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16>(a, L, to_end, stream)
-                                 : launch_stream_x<XF32>(a, L, to_end, stream);
+  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, stream)
+                                 : launch_stream_x<XF32, true>(a, L, to_end, stream);
 }
 
 }  // namespace fwd

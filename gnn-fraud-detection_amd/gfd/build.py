@@ -36,10 +36,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-at
          f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
 # GFD_EXTRA_FLAGS: A/B builds into their own library (with GFD_BUILD_VARIANT)
 FLAGS += os.environ.get("GFD_EXTRA_FLAGS", "").split()
-# Per-source flags.  k_mid runs 16 waves at <= 128 VGPRs: the SLP vectoriser's
-# packed-pair copies of the gathered rows push it into scratch (rows spilled
-# right after their loads), scalar FMAs with SGPR-broadcast weights do not.
-SOURCE_FLAGS = {"gfd_mid.hip": ["-fno-slp-vectorize"]}
+# Per-source flags (none at present): {"file.hip": [flags]}
+SOURCE_FLAGS = {}
 
 
 def sources():
