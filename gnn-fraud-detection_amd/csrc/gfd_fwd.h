@@ -236,6 +236,23 @@ __device__ __forceinline__ int pack_zrow(const f32x2 (&z)[4][KF], float inv, int
   return er;
 }
 
+// Split an already normalised and scaled z row into fp16 hi / lo'.
+template <int KF>
+__device__ __forceinline__ void split_zrow(const f32x2 (&z)[4][KF], f16x8 (&hi)[KF],
+                                           f16x8 (&lo)[KF]) {
+#pragma unroll
+  for (int qq = 0; qq < KF; ++qq) {
+    union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } a, b;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      a.p[g] = __builtin_convertvector(z[g][qq], f16x2);
+      b.u[g] = split_lo(z[g][qq], a.u[g]);
+    }
+    hi[qq] = a.v;
+    lo[qq] = b.v;
+  }
+}
+
 // Store a packed row into a Z tile (one 16-B write per feature and plane).
 template <int KF>
 __device__ __forceinline__ void write_zrow(const f16x8 (&hi)[KF], const f16x8 (&lo)[KF], int Fp,
@@ -319,14 +336,23 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
     for (int k0 = 0; k0 < nk; k0 += 4) {  // sub-batches of 4 rows, loads issued together
       float xv[4][KF];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * (k0 + k)), ldx), F, lane,
-                         k0 + k < nk, xv[k]);
+      for (int k = 0; k < 4; ++k) {
+        // clamped plain loads (f >= F reads x[F - 1] and selects 0: never the
+        // row padding); 0.37 ms faster at C4 than per-row buffer descriptors
+        const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
+            xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * (k0 + k)), ldx));
+#pragma unroll
+        for (int q = 0; q < KF; ++q) {
+          const int f = lane + 64 * q;
+          const float t = xcvt(xr[f < F ? f : F - 1]);
+          xv[k][q] = f < F ? t : 0.f;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
 #pragma unroll
         for (int hh = 0; hh < H; ++hh) {
-          // p of a padding message is 0 and its row reads as zeros
+          // p of a padding message is 0 (its clamped row is a valid one)
           const float pk =
               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 8 * (k0 + k) + hh));
 #pragma unroll

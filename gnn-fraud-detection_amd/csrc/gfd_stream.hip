@@ -47,7 +47,12 @@ using namespace gfd::fwd;
 namespace {
 
 constexpr int kSWaves = 8;
-constexpr int kAP = 2;  // A-fragment k-steps read ahead in the MFMA loop
+#ifndef GFD_LIGHT_AP
+#define GFD_LIGHT_AP 2
+#endif
+// A-fragment k-steps read ahead in the MFMA loop (general, light)
+template <bool LIGHT>
+constexpr int ap_of() { return LIGHT ? GFD_LIGHT_AP : 2; }
 
 struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm queue)
   int v;          // lanes 0..3: {row, e_begin, e_end, hub_rank}; lanes 8..15: sources of
@@ -161,11 +166,20 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF>& q, in
   }
   const float inv = __builtin_amdgcn_rcpf(l + kSoftmaxEps);
   f32x2 z[4][KF];
-  if (kmax <= 1) fma_k<KF, 1>(z, q.xv, p);
-  else if (kmax == 2) fma_k<KF, 2>(z, q.xv, p);
-  else fma_k<KF, 4>(z, q.xv, p);
   f16x8 hi[KF], lo[KF];
-  const int er = pack_zrow<KF>(z, inv, erg, hi, lo);
+  int er = erg;
+  if (erg != 127) {
+    // one scale for every row: fold 1 / (sum + eps) and 2^erg into the
+    // weights, so z comes out normalised and scaled and only needs the split
+    const float ps = p * (inv * ldexpf(1.0f, erg));
+    if (kmax <= 2) fma_k<KF, 2>(z, q.xv, ps);
+    else fma_k<KF, 4>(z, q.xv, ps);
+    split_zrow<KF>(z, hi, lo);
+  } else {
+    if (kmax <= 2) fma_k<KF, 2>(z, q.xv, p);
+    else fma_k<KF, 4>(z, q.xv, p);
+    er = pack_zrow<KF>(z, inv, erg, hi, lo);
+  }
   write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
   if (lane == 0) {
     rsc[r] = ldexpf(1.0f, -er);
@@ -421,6 +435,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     // A fragments (and LDS-resident W_lo) kAP k-steps ahead; the scheduling
     // barriers keep the compiler from hoisting every LDS read of the tile
     // (registers belong to W)
+    constexpr int kAP = ap_of<LIGHT>();
     f16x8 phi[kAP], plo[kAP], pwl[kAP];
 #pragma unroll
     for (int u = 0; u < kAP; ++u) {
