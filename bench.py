@@ -325,7 +325,8 @@ def measure(args, dev, rank, world, config):
                          "frac": gbps / HBM_PEAK_GBPS}
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
     kname = {"pack+logits": "k_logits_s (+ pack)", "hubs": "k_hub_partial + k_hub_fin",
-             "general": "k_mid (general tiles)", "light": "k_stream (light tiles)",
+             "general": "k_stream<general> (hub rows, 5+ messages)",
+             "light": "k_stream<light> (2-4 messages)",
              "lone": "k_lone (self-loop-only rows)"}
     pmc = load_pmc(args.pmc, f"{config}:{dom}:N={N}:E={E}:F={F}:world={world}")
     workload = (f"{config.upper()} power-law N={N} E={E} F={F} gamma={args.gamma} "

@@ -193,13 +193,13 @@ size_t fused_smem(int Fp) {  // fp16 hi + lo half-tile (= 4 B per element) + par
   return sizeof(float) * (kTile * (4 * Fp + 8) + 3 * 4 * 64 * 4 + 2 * kTile);
 }
 
-// KF <= 2 fits 64 VGPRs (8 waves per SIMD, two blocks per CU); KF >= 3 runs at
-// 4 waves per SIMD (at 64 VGPRs it spilled ~52 B/lane per destination).
+// KF = 1 fits 64 VGPRs (8 waves per SIMD, two blocks per CU); KF >= 2 (two
+// batches of rows in flight in aggregate_segment) runs at 4 waves per SIMD.
 template <typename XT, int KF>
 gfd_status launch_fused_t(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
   const gfd_plan& p = a.plan;
   const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
-  auto kern = KF >= 3 ? &k_fused<XT, KF, 4> : &k_fused<XT, KF, 8>;
+  auto kern = KF >= 2 ? &k_fused<XT, KF, 4> : &k_fused<XT, KF, 8>;
   kern<<<int(tiles), kFusedWaves * 64, fused_smem(L.Fp), stream>>>(
       a.x, a.F, L.Fp, a.ldx, a.rowptr, a.col, a.num_dst, a.dst_offset, p.row_order,
       reinterpret_cast<const int4*>(p.slot_desc), a.st,

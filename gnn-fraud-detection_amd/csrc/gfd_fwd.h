@@ -292,7 +292,9 @@ __device__ __forceinline__ void fma_rows(f32x2 (&z)[4][KF], const float (&xr)[NR
 // online softmax.  Logit lane layout: lane = 8 k + h (message k of a batch of
 // 8, head h); aggregation lane layout: lane <-> feature f = lane + 64 q.
 // Returns the running max (head lane & 7) and the denominator; acc[h][q] =
-// sum_j p_jh x_j[f] relative to that max.
+// sum_j p_jh x_j[f] relative to that max.  (Measured at C4: the hub chunks
+// run at ~5 TB/s with one batch in flight per wave at 5 waves per SIMD;
+// keeping a second batch in flight cost occupancy and time.)
 struct SegState {
   float m;
   float ssum;
@@ -317,44 +319,43 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
     const bool valid = e < e1;
     const int j = col[valid ? e : e1 - 1];  // clamped: every load is in bounds
     const float v = leaky(st[int64_t(j) * 16 + h] + t_h, slope);
-    const float bm = max_xor8_16_32(valid ? v : -INFINITY);
-    const float mn = fmaxf(m, bm);
+    const float mn = fmaxf(m, max_xor8_16_32(valid ? v : -INFINITY));
     const float sc = __expf(m - mn);  // 0 on the first batch, 1 while the max holds
     float p = valid ? __expf(v - mn) : 0.f;
     l = fmaf(l, sc, p);
     if (b != e0 && __any(sc != 1.0f)) {  // wave-uniform: rescale the running sums
 #pragma unroll
       for (int hh = 0; hh < H; ++hh) {
-        const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
+        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
 #pragma unroll
-        for (int q = 0; q < KF; ++q) acc[hh][q] *= s;
+        for (int q = 0; q < KF; ++q) acc[hh][q] *= r;
       }
     }
     m = mn;
     if (dp > 0.f) p = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? p * keep_scale : 0.f;
+    // all 8 rows of the batch issued together; clamped plain loads (f >= F
+    // reads x[F - 1] and selects 0: never the row padding)
     const int nk = min(8, e1 - b);
-    for (int k0 = 0; k0 < nk; k0 += 4) {  // sub-batches of 4 rows, loads issued together
-      float xv[4][KF];
+    float xv[8][KF];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        // clamped plain loads (f >= F reads x[F - 1] and selects 0: never the
-        // row padding); 0.37 ms faster at C4 than per-row buffer descriptors
-        const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
-            xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * (k0 + k)), ldx));
+    for (int k = 0; k < 8; ++k) {
+      const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
+          xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * k), ldx));
 #pragma unroll
-        for (int q = 0; q < KF; ++q) {
-          const int f = lane + 64 * q;
-          const float t = xcvt(xr[f < F ? f : F - 1]);
-          xv[k][q] = f < F ? t : 0.f;
-        }
+      for (int q = 0; q < KF; ++q) {
+        const int f = lane + 64 * q;
+        const float t = xcvt(xr[f < F ? f : F - 1]);
+        xv[k][q] = f < F ? t : 0.f;
       }
+    }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
+      if (k < nk) {
 #pragma unroll
         for (int hh = 0; hh < H; ++hh) {
           // p of a padding message is 0 (its clamped row is a valid one)
           const float pk =
-              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 8 * (k0 + k) + hh));
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 8 * k + hh));
 #pragma unroll
           for (int q = 0; q < KF; ++q) acc[hh][q] = fmaf(pk, xv[k][q], acc[hh][q]);
         }
