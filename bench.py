@@ -59,6 +59,10 @@ def parse(argv=None):
     p.add_argument("--gamma", type=float, default=2.1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-legs", action="store_true")
+    p.add_argument("--legs", default="c4bwd,c5,c1,c2,c3",
+                   help="comma list of legs run after the headline line (N = 1)")
+    p.add_argument("--legs-only", action="store_true",
+                   help="skip the C4 headline timing (development)")
     p.add_argument("--cpu-messages", type=int, default=3_000_000,
                    help="messages in the CPU-baseline sample of the C4 graph")
     p.add_argument("--cpu-runs", type=int, default=3)
@@ -310,6 +314,8 @@ def measure(args, dev, rank, world, config):
         f"shard=[{s['spec'].dst_lo},{s['spec'].dst_hi}) hubs={plan.num_hubs} "
         f"chunks={plan.num_chunks} classes={plan.classes()} "
         f"setup {time.perf_counter() - t_setup:.1f}s")
+    if getattr(args, "legs_only", False) and config == "c4":
+        return {"legs_only": True}, s, layer
     elapsed, stage_ms = time_layer(layer, args.steps, args.warmup, world)
     ms_step = elapsed * 1e3 / args.steps
     value = E * args.steps / elapsed
@@ -370,13 +376,18 @@ def main():
     torch.cuda.set_device(dev)
     res, s, layer = measure(args, dev, rank, world, args.config)
     if world == 1 and rank == 0 and args.config == "c4":
-        if not args.no_cpu_baseline:
+        import bench_legs
+        want = [w for w in args.legs.split(",") if w] if not args.no_legs else []
+        legs = {}
+        if not args.no_cpu_baseline and not args.legs_only:
             log("[bench] timing CPU baseline (oracle, bounded sample of the C4 graph) ...")
             res["cpu_baseline"] = cpu_baseline(s, args)
+        if "c4bwd" in want:
+            log("[bench] leg C4 forward + backward ...")
+            legs["c4_layer_fwd_bwd"] = bench_legs.c4_layer_fwd_bwd(s, dev)
         del s, layer
         torch.cuda.empty_cache()
-        if not args.no_legs:
-            legs = {}
+        if "c5" in want:
             log("[bench] leg C5: bf16 features, 50M nodes / 500M edges ...")
             c5, s5, l5 = measure(args, dev, 0, 1, "c5")
             del s5, l5
@@ -384,6 +395,13 @@ def main():
             legs["c5_bf16_forward"] = {k: c5[k] for k in ("metric", "value", "unit", "ms_per_step",
                                                           "dtype", "config", "roofline",
                                                           "kernels", "layer")}
+        for name, fn in (("c1", "c1_gat2_forward"), ("c2", "c2_gat3_train_step"),
+                         ("c3", "c3_tgn_49_steps")):
+            if name in want:
+                log(f"[bench] leg {fn} ...")
+                legs[fn] = getattr(bench_legs, fn)(dev)
+                torch.cuda.empty_cache()
+        if legs:
             res["legs"] = legs
     if rank == 0:
         print(json.dumps(res), flush=True)

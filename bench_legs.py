@@ -1,0 +1,150 @@
+"""bench_legs.py -- the secondary BASELINE.json configurations, reported under
+``legs`` of bench.py's JSON line (N = 1 only).  Each leg times the product path
+(libgfd.so through gfd.models / gfd.nn) with HIP events around whole steps.
+
+* ``c1_gat2_forward``   -- configs[0]: the reference's 2-layer GAT forward on
+  the Elliptic-shaped graph (203,769 nodes / 234,355 edges / 165 features),
+  HIP vs the oracle's PyG CPU dataflow (GATRef) on the same weights and graph.
+* ``c2_gat3_train_step`` -- configs[1]: one training step of the reference
+  loop (train.py:103-145): zero_grad, 3-layer GAT forward (train mode,
+  dropout 0.2), masked BCEWithLogits(pos_weight=50), backward, Adam
+  (lr 1e-3, weight decay 5e-4; config.py:36-44).
+* ``c3_tgn_49_steps``   -- configs[2]: TemporalGNN (3 layers) forward over the
+  49 time-step snapshots, eval mode.
+* ``c4_layer_fwd_bwd``   -- the C4 layer-0 GATConv forward + backward (no
+  grad_x: layer-0 features are data), the training cost at C4 scale.
+
+Synthetic data only (gfd.synth; the Elliptic CSVs are not in the reference).
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+H, C = 8, 64
+
+
+def _events(n):
+    return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+
+
+def _time(fn, steps, warmup):
+    """Median and mean ms of ``fn`` over ``steps`` runs (after ``warmup``)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = _events(steps + 1)
+    ev[0].record()
+    for k in range(steps):
+        fn()
+        ev[k + 1].record()
+    torch.cuda.synchronize()
+    ms = sorted(ev[k].elapsed_time(ev[k + 1]) for k in range(steps))
+    return ms[len(ms) // 2], ev[0].elapsed_time(ev[-1]) / steps
+
+
+def _elliptic(dev, F=165, seed=0):
+    from gfd import synth
+    d = synth.elliptic_like(num_features=F, seed=seed)
+    return {"x": torch.from_numpy(d["x"]).to(dev), "edge_index": torch.from_numpy(d["edge_index"]).to(dev),
+            "time_step": torch.from_numpy(d["time_step"]).to(dev), "y": torch.from_numpy(d["y"]).to(dev),
+            "E": d["edge_index"].shape[1], "N": d["x"].shape[0]}
+
+
+def _model(kind, F, layers, dev, seed=0, dropout=0.2):
+    from gfd.models import GAT, TemporalGNN
+    torch.manual_seed(seed)
+    cls = GAT if kind == "gat" else TemporalGNN
+    return cls(in_channels=F, hidden_channels=64, out_channels=1, num_layers=layers,
+               dropout=dropout).to(dev)
+
+
+def c1_gat2_forward(dev, steps=20, warmup=3, cpu_runs=3):
+    from oracle import GATRef
+    d = _elliptic(dev)
+    m = _model("gat", 165, 2, dev).eval()
+    with torch.no_grad():
+        med, mean = _time(lambda: m(d["x"], d["edge_index"]), steps, warmup)
+        out = m(d["x"], d["edge_index"])
+    ref = GATRef(165, 64, 1, num_layers=2).eval()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=True)
+    xc, ec = d["x"].cpu(), d["edge_index"].cpu()
+    times = []
+    with torch.no_grad():
+        for _ in range(1 + cpu_runs):
+            t0 = time.perf_counter()
+            rout = ref(xc, ec)
+            times.append(time.perf_counter() - t0)
+    tt = sorted(times[1:])
+    err = (out.cpu() - rout).abs().max().item()
+    return {"workload": f"GAT 2 layers (165 -> 64, 8 heads), Elliptic-shaped N={d['N']} "
+                        f"E={d['E']}, eval forward", "unit": "edges/s",
+            "value": d["E"] / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
+            "cpu_baseline": {"value": d["E"] / tt[len(tt) // 2], "unit": "edges/s",
+                             "median_s": tt[len(tt) // 2], "min_s": tt[0], "runs": cpu_runs,
+                             "cores": torch.get_num_threads(), "kind": "port",
+                             "sample": "the whole C1 graph: oracle GATRef (PyG CPU dataflow)"},
+            "max_abs_err_vs_oracle": err}
+
+
+def c2_gat3_train_step(dev, steps=20, warmup=3):
+    d = _elliptic(dev)
+    m = _model("gat", 165, 3, dev).train()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=5e-4)
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0], device=dev))
+    mask = d["y"] != -1
+    yl = d["y"][mask].float()
+
+    def step():
+        opt.zero_grad()
+        logits = m(d["x"], d["edge_index"])
+        loss = crit(logits[mask].squeeze(1), yl)
+        loss.backward()
+        opt.step()
+
+    med, mean = _time(step, steps, warmup)
+    fwd_med, _ = _time(lambda: m(d["x"], d["edge_index"]), steps, warmup)
+    return {"workload": f"GAT 3 layers train step (fwd + BCE(pos_weight 50) + bwd + Adam), "
+                        f"Elliptic-shaped N={d['N']} E={d['E']} F=165, dropout 0.2",
+            "unit": "edges/s", "value": d["E"] / (med * 1e-3), "ms_per_step": med,
+            "ms_mean": mean, "forward_ms_train_mode": fwd_med}
+
+
+def c3_tgn_49_steps(dev, steps=20, warmup=3):
+    d = _elliptic(dev)
+    m = _model("tgn", 165, 3, dev).eval()
+    with torch.no_grad():
+        med, mean = _time(lambda: m.forward_snapshots(d["x"], d["edge_index"], d["time_step"]),
+                          steps, warmup)
+    return {"workload": f"TemporalGNN 3 layers, forward over the 49 time-step snapshots "
+                        f"(h0 = 0 per step), N={d['N']} E={d['E']} F=165, eval",
+            "unit": "edges/s", "value": d["E"] / (med * 1e-3), "ms_per_step": med,
+            "ms_mean": mean}
+
+
+def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2):
+    """GATConv forward + backward on the C4 workload ``s`` (bench.setup)."""
+    from gfd.nn import gat_conv
+    W = s["W"].clone().requires_grad_(True)
+    a_s = s["a_s"].clone().requires_grad_(True)
+    a_d = s["a_d"].clone().requires_grad_(True)
+    b = s["bias"].clone().requires_grad_(True)
+    g = s["graph"]
+    grad = torch.randn((g.num_nodes, C), device=dev, generator=torch.Generator(device=dev).manual_seed(4))
+    g.csc()
+
+    def fwd():
+        return gat_conv(s["x"], g, W, a_s, a_d, b, training=True)
+
+    def fwd_bwd():
+        out = fwd()
+        out.backward(grad)
+
+    fwd_med, _ = _time(lambda: fwd(), steps, warmup)
+    med, mean = _time(fwd_bwd, steps, warmup)
+    E = s["graph"].num_messages - s["graph"].num_nodes
+    return {"workload": f"C4 GATConv layer 0 forward (training stats) + backward (grad W, att, "
+                        f"bias; no grad_x), N={g.num_nodes} E={E}", "unit": "edges/s",
+            "value": E / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
+            "forward_ms": fwd_med, "backward_ms": med - fwd_med}

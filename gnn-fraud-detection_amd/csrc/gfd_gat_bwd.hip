@@ -1,62 +1,616 @@
 // gfd_gat_bwd.hip -- GATConv backward for gfx950 (the autograd of PyG's
 // GATConv dataflow that the reference runs at loss.backward(), train.py:142;
-// formulas: SURVEY.md Appendix A).
+// formulas: SURVEY.md Appendix A).  Like the forward it never forms the
+// 512-wide projected rows h = x W^T: with g_i = dL/dout_i,
 //
-//   k_gemm (fp32 MFMA 16x16x4, exact fp32 chains)  h = x W^T          [N, H*C]
-//   k_bwd_dst   one wave per destination i (CSR): recompute alpha from the
-//               saved (s, t, max, sum); dA = <g_i, h_jh>/H; softmax backward
-//               -> dpre per message; dt_i; grad_bias
-//   k_bwd_src   one wave per source j (CSC): ds_j = sum dpre; y_jh = sum
-//               alpha_d g_i; dh_j = y/H + ds a_src + dt a_dst; grad_att_*
-//   k_gemm      grad_x = dh W ;  grad_W = dh^T x (split-K over nodes)
-#include "gfd_common.h"
+//   dA_ijh  = <g_i, W_h x_j> / H = <u_ih, x_j>,   u_ih = W_h^T g_i / H   (F wide)
+//   dpre    = alpha (dA - sum_j alpha dA) leaky'(pre)   (softmax + leaky backward)
+//   dt_ih   = sum_j dpre_ijh          ds_jh = sum_i dpre_ijh
+//   y_jh    = sum_i alpha~_ijh g_i    (alpha~ = alpha after dropout)
+//   dh_jh   = y_jh / H + ds_jh a_src,h + dt_jh a_dst,h     (dL/dh_jh)
+//   grad_W  = sum_j dh_j x_j^T,  grad_att_src,h = W_h S_h, S_h = sum_j ds_jh x_j
+//                                grad_att_dst,h = W_h T_h, T_h = sum_i dt_ih x_i
+//   grad_x  = dh W,  grad_bias = sum_i g_i
+//
+// Kernels
+//   k_bwd_msg     32 destinations per block (16 waves): U = G W on f16 MFMA
+//                 (3-term hi/lo split, W fragments from L2) -> LDS -> each wave
+//                 holds u_i (8 x F) in registers and walks its destinations'
+//                 messages: x_j gathered once (664 B at F = 166, not the 2 KB
+//                 h_j row), 8 head dots, a transposing 64-lane reduce, softmax
+//                 backward in a second sweep.  Hub rows park u_i for:
+//   k_bwd_hub1/2  hub chunks (the forward plan's split), chunk partials summed
+//                 in a fixed order by k_sum8
+//   k_bwd_src     one wave per source (CSC), chunks for source hubs: writes
+//                 dh' = [dh (512) | ds (8) | dt (8)] per node
+//   k_gemm_tn     grad_W' = dh'^T x (528 x F), split-K slabs + ordered reduce
+//   k_att_grad    grad_att from the S / T rows of grad_W'
+//   k_gemm        grad_x = dh W (only when requested)
+// Deterministic: no float atomics anywhere; every sum has a fixed order.
+#include "gfd_fwd.h"
 
 using namespace gfd;
+using namespace gfd::fwd;
 
 namespace {
 
-constexpr int H = kHeads;
-constexpr int C = kChannels;
 constexpr int HC = H * C;
+constexpr int kDH = HC + 2 * H;    // dh' row: dh (512) | ds (8) | dt (8)
+constexpr int kUT = 32;            // destinations per k_bwd_msg block
+constexpr int kUW = 16;            // waves per k_bwd_msg block
+constexpr int kGS = 72;            // G tile row stride (halves; 144 B rows keep 16-B loads aligned)
+constexpr int kRedBlocks = 1024;   // fixed grid of the column-sum partial kernels
+
+__device__ __forceinline__ float ldx1(const float* p) { return *p; }
+__device__ __forceinline__ float ldx1(const uint16_t* p) { return __uint_as_float(uint32_t(*p) << 16); }
 
 // ---------------------------------------------------------------------------
-// Generic strided fp32 GEMM on v_mfma_f32_16x16x4_f32:
-//   Cm(m, n) (+)= sum_k A(m, k) B(k, n);  X(r, c) = X[r * s_r + c * s_c]
-// 64x64 block tile, BK = 16, 4 waves of 32x32; split-K over gridDim.z with
-// float atomics into a zeroed C when gridDim.z > 1.
+// Transposing 64-lane reduce of 8 per-head values: returns, in every lane of
+// octet o (= lane >> 3), the sum over all 64 lanes of v[o].  Three swap steps
+// (permlane32 / permlane16 / row_ror:8) halve the values per lane, then a DPP
+// octet sum.
+__device__ __forceinline__ float treduce8(float (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {  // lane bit 5 <- head bit 2
+    auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[h]), __float_as_uint(v[h + 4]),
+                                              false, false);
+    v[h] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // lane bit 4 <- head bit 1
+    auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[h]), __float_as_uint(v[h + 2]),
+                                              false, false);
+    v[h] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  }
+  const bool up = (lane & 8) != 0;  // lane bit 3 <- head bit 0
+  const float send = up ? v[0] : v[1];
+  float r = (up ? v[1] : v[0]) + dpp_mov<0x128>(send);  // row_ror:8 = lane ^ 8
+  r += dpp_mov<0xB1>(r);                                // quad_perm [1,0,3,2]
+  r += dpp_mov<0x4E>(r);                                // quad_perm [2,3,0,1]
+  r += dpp_mov<0x141>(r);                               // row_half_mirror
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Pass 1 over the messages [e0, e1) of destination i (logit lane layout lane =
+// 8 k + h): dA = <u_ih, x_j> (times the dropout keep factor) and alpha~ to the
+// per-message buffers; returns sum_j alpha dA for head lane & 7 (all lanes).
+template <typename XT, int KF>
+__device__ __forceinline__ float bwd_pass1(const void* __restrict__ x, int64_t ldx, int F,
+                                           const int32_t* __restrict__ col, int e0, int e1,
+                                           const float* __restrict__ st, float t_h, float m_h,
+                                           float inv_h, const float (&u)[H][KF], float slope,
+                                           float dp, uint64_t seed, float* __restrict__ dpre,
+                                           float* __restrict__ alpha_d) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  const int sig = (8 * h + kk) * 4;  // transpose (k, h) -> (h, k) for the bpermute
+  const float keep_scale = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+  float adot = 0.f;
+  for (int b = e0; b < e1; b += 8) {
+    const int e = b + kk;
+    const bool valid = e < e1;
+    const int j = col[valid ? e : e1 - 1];
+    const float pre = st[int64_t(j) * 16 + h] + t_h;
+    const float al = __expf(leaky(pre, slope) - m_h) * inv_h;
+    float keepf = 1.0f;
+    if (dp > 0.f) keepf = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? keep_scale : 0.f;
+    const int nk = min(8, e1 - b);
+    float xv[8][KF];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
+          xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * k), ldx));
+#pragma unroll
+      for (int q = 0; q < KF; ++q) {
+        const int f = lane + 64 * q;
+        const float t = xcvt(xr[f < F ? f : F - 1]);
+        xv[k][q] = f < F ? t : 0.f;
+      }
+    }
+    float sel = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < nk) {
+        float v[8];
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {
+          float s = u[hh][0] * xv[k][0];
+#pragma unroll
+          for (int q = 1; q < KF; ++q) s = fmaf(u[hh][q], xv[k][q], s);
+          v[hh] = s;
+        }
+        const float r = treduce8(v);  // lane 8 o + *: message k, head o
+        sel = (lane & 7) == k ? r : sel;
+      }
+    }
+    // lane 8 k + h <- lane 8 h + k (message k, head h)
+    const float dA = __int_as_float(__builtin_amdgcn_ds_bpermute(sig, __float_as_int(sel))) * keepf;
+    if (valid) {
+      dpre[int64_t(e) * 8 + h] = dA;
+      alpha_d[int64_t(e) * 8 + h] = al * keepf;
+      adot = fmaf(al, dA, adot);
+    }
+  }
+  return sum_xor8_16_32(adot);
+}
+
+// Pass 2: dpre = alpha (dA - adot) leaky'(pre) in place; returns dt (head lane & 7).
+__device__ __forceinline__ float bwd_pass2(const int32_t* __restrict__ col, int e0, int e1,
+                                           const float* __restrict__ st, float t_h, float m_h,
+                                           float inv_h, float adot, float slope,
+                                           float* __restrict__ dpre) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  float dts = 0.f;
+  for (int b = e0; b < e1; b += 8) {
+    const int e = b + kk;
+    if (e < e1) {
+      const int j = col[e];
+      const float pre = st[int64_t(j) * 16 + h] + t_h;
+      const float al = __expf(leaky(pre, slope) - m_h) * inv_h;
+      float* dp = dpre + int64_t(e) * 8 + h;
+      const float d = al * (*dp - adot) * (pre > 0.f ? 1.0f : slope);
+      *dp = d;
+      dts += d;
+    }
+  }
+  return sum_xor8_16_32(dts);
+}
+
+__device__ __forceinline__ void mfma_split(const _Float16* __restrict__ ah,
+                                           const _Float16* __restrict__ al, const uint4& bh,
+                                           const uint4& bl, f32x4& acc_m, f32x4& acc_x) {
+  const f16x8 a_h = *reinterpret_cast<const f16x8*>(ah);
+  const f16x8 a_l = *reinterpret_cast<const f16x8*>(al);
+  const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+  const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+  acc_m = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, b_h, acc_m, 0, 0, 0);
+  acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, b_l, acc_x, 0, 0, 0);
+  acc_x = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l, b_h, acc_x, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// W fragments for U_h = G W_h (B operand [K = 64 channels, N = Fu features]):
+// fragment ((h * 2 + s) * NT + ct), lane l holds W_h[32 s + 8 (l >> 4) + t][16 ct
+// + (l & 15)], t = 0..7, scaled by 2^kw (max |W| -> [2^13, 2^14)); lo' =
+// (w - hi) 2^11.  whdr[0] = 2^-kw.
+__global__ void __launch_bounds__(1024) k_bwd_wmax(const float* __restrict__ W, int n,
+                                                   float* __restrict__ whdr) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(W[i]));
+  m = max_wave(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = red[0];
+    for (int i = 1; i < 16; ++i) t = fmaxf(t, red[i]);
+    const int kw = scale_exp(t);
+    whdr[0] = ldexpf(1.0f, -kw);
+    whdr[1] = ldexpf(1.0f, kw);
+  }
+}
+
+__global__ void k_bwd_wpack(const float* __restrict__ W, int F, int NT,
+                            const float* __restrict__ whdr, uint4* __restrict__ bhi,
+                            uint4* __restrict__ blo) {
+  const int64_t idx = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (idx >= int64_t(H) * 2 * NT * 64) return;
+  const int lane = int(idx & 63);
+  const int64_t fr = idx >> 6;
+  const int ct = int(fr % NT), s = int((fr / NT) & 1), h = int(fr / (2 * NT));
+  const float sc = whdr[1];
+  const int f = 16 * ct + (lane & 15);
+  union { _Float16 e[8]; uint4 u; } hi, lo;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int c = 32 * s + 8 * (lane >> 4) + t;
+    const float w = f < F ? W[int64_t(h * C + c) * F + f] * sc : 0.f;
+    const _Float16 wh = (_Float16)w;
+    hi.e[t] = wh;
+    lo.e[t] = (_Float16)((w - (float)wh) * kLoScale);
+  }
+  bhi[idx] = hi.u;
+  blo[idx] = lo.u;
+}
+
+// ---------------------------------------------------------------------------
+template <typename XT, int KF>
+__global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
+    const void* __restrict__ x, int F, int Fu, int64_t ldx, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, int64_t n_dst, const int4* __restrict__ desc,
+    const int32_t* __restrict__ hub_rank, const float* __restrict__ st,
+    const float* __restrict__ stats, const float* __restrict__ g, const float* __restrict__ whdr,
+    const uint4* __restrict__ bhi, const uint4* __restrict__ blo, float slope, float dp,
+    uint64_t seed, float* __restrict__ uhub, float* __restrict__ dpre,
+    float* __restrict__ alpha_d, float* __restrict__ dt) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  _Float16* Gh = reinterpret_cast<_Float16*>(smem);        // [32][kGS]
+  _Float16* Gl = Gh + kUT * kGS;                          // [32][kGS]
+  float* rsc = reinterpret_cast<float*>(Gl + kUT * kGS);  // [32] row unscale
+  float* U = rsc + kUT;                                   // [32][4][Fu]
+  const int lane = threadIdx.x & 63;
+  const int w = wave_uniform(threadIdx.x >> 6);
+  const int64_t base = int64_t(blockIdx.x) * kUT;
+
+  int4 dsc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const int64_t slot = base + w + 16 * d;
+    dsc[d] = make_int4(-1, 0, 0, -1);
+    if (slot < n_dst) {
+      if (desc) {
+        dsc[d] = uni4(desc[slot]);
+      } else {
+        const int r = int(slot);
+        dsc[d] = make_int4(r, rowptr[r], rowptr[r + 1], hub_rank ? hub_rank[r] : -1);
+      }
+    }
+    // G row: power-of-two scaled, fp16 hi / lo'
+    const int i = dsc[d].x;
+    const float gv = i >= 0 ? g[int64_t(i) * C + lane] : 0.f;
+    const int er = scale_exp(max_wave(fabsf(gv)));
+    const float t = gv * ldexpf(1.0f, er);
+    const _Float16 th = (_Float16)t;
+    const int row = w + 16 * d;
+    Gh[row * kGS + lane] = th;
+    Gl[row * kGS + lane] = (_Float16)((t - (float)th) * kLoScale);
+    if (lane == 0) rsc[row] = ldexpf(1.0f, -er) * whdr[0] * (1.0f / H);
+  }
+  __syncthreads();
+
+  // U = G W (two head groups of 4), then each wave keeps its rows' u_i
+  const int NT = Fu / 16;
+  float u[2][H][KF];
+#pragma unroll
+  for (int hg = 0; hg < 2; ++hg) {
+    for (int p = w; p < 4 * NT; p += kUW) {
+      const int hl = p / NT, ct = p - hl * NT, h = 4 * hg + hl;
+      f32x4 am[2], ax[2];
+#pragma unroll
+      for (int rg = 0; rg < 2; ++rg) am[rg] = ax[rg] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int64_t fi = (int64_t(h * 2 + s) * NT + ct) * 64 + lane;
+        const uint4 bh = bhi[fi], bl = blo[fi];
+#pragma unroll
+        for (int rg = 0; rg < 2; ++rg) {
+          const int ao = (16 * rg + (lane & 15)) * kGS + 32 * s + 8 * (lane >> 4);
+          mfma_split(Gh + ao, Gl + ao, bh, bl, am[rg], ax[rg]);
+        }
+      }
+#pragma unroll
+      for (int rg = 0; rg < 2; ++rg) {
+        const f32x4 acc = am[rg] + ax[rg] * (1.0f / kLoScale);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 16 * rg + 4 * (lane >> 4) + q;
+          U[(row * 4 + hl) * Fu + 16 * ct + (lane & 15)] = acc[q] * rsc[row];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int hl = 0; hl < 4; ++hl)
+#pragma unroll
+        for (int q = 0; q < KF; ++q) {
+          const int f = lane + 64 * q;
+          u[d][4 * hg + hl][q] = f < Fu ? U[((w + 16 * d) * 4 + hl) * Fu + f] : 0.f;
+        }
+    __syncthreads();
+  }
+
+  // messages of this wave's two destinations
+  const int h = lane & 7;
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const int i = dsc[d].x;
+    if (i < 0) continue;
+    if (dsc[d].w >= 0) {  // hub: its chunks run in k_bwd_hub1 / 2 with this u_i
+      float* ur = uhub + int64_t(dsc[d].w) * H * Fu;
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+        for (int q = 0; q < KF; ++q) {
+          const int f = lane + 64 * q;
+          if (f < Fu) ur[hh * Fu + f] = u[d][hh][q];
+        }
+      continue;
+    }
+    const float t_h = st[int64_t(i) * 16 + H + h];
+    const float m_h = stats[int64_t(i) * 16 + h];
+    const float inv_h = 1.0f / (stats[int64_t(i) * 16 + H + h] + kSoftmaxEps);
+    const float adot = bwd_pass1<XT, KF>(x, ldx, F, col, dsc[d].y, dsc[d].z, st, t_h, m_h, inv_h,
+                                         u[d], slope, dp, seed, dpre, alpha_d);
+    const float dts = bwd_pass2(col, dsc[d].y, dsc[d].z, st, t_h, m_h, inv_h, adot, slope, dpre);
+    if (lane < 8) dt[int64_t(i) * 8 + lane] = dts;
+  }
+}
+
+size_t msg_smem(int Fu) {
+  return sizeof(_Float16) * 2 * kUT * kGS + sizeof(float) * (kUT + kUT * 4 * size_t(Fu));
+}
+
+// Hub chunks {hub, e0, e1, dst}, one wave each.  Pass 1 -> cpart[c][8] = partial adot.
+template <typename XT, int KF>
+__global__ void __launch_bounds__(256) k_bwd_hub1(
+    const void* __restrict__ x, int F, int Fu, int64_t ldx, const int32_t* __restrict__ col,
+    const float* __restrict__ st, const float* __restrict__ stats, const float* __restrict__ uhub,
+    const int4* __restrict__ chunks, int64_t num_chunks, float slope, float dp, uint64_t seed,
+    float* __restrict__ dpre, float* __restrict__ alpha_d, float* __restrict__ cpart) {
+  const int lane = threadIdx.x & 63, h = lane & 7;
+  const int64_t c = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  if (c >= num_chunks) return;
+  const int4 ck = uni4(chunks[c]);
+  float u[H][KF];
+  const float* ur = uhub + int64_t(ck.x) * H * Fu;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < KF; ++q) {
+      const int f = lane + 64 * q;
+      u[hh][q] = f < Fu ? ur[hh * Fu + f] : 0.f;
+    }
+  const int64_t i = ck.w;
+  const float t_h = st[i * 16 + H + h];
+  const float m_h = stats[i * 16 + h];
+  const float inv_h = 1.0f / (stats[i * 16 + H + h] + kSoftmaxEps);
+  const float a = bwd_pass1<XT, KF>(x, ldx, F, col, ck.y, ck.z, st, t_h, m_h, inv_h, u, slope, dp,
+                                    seed, dpre, alpha_d);
+  if (lane < 8) cpart[c * 8 + lane] = a;
+}
+
+// Pass 2 of a hub chunk with the hub's total adot -> cpart[c][8] = partial dt.
+__global__ void __launch_bounds__(256) k_bwd_hub2(const int32_t* __restrict__ col,
+                                                  const float* __restrict__ st,
+                                                  const float* __restrict__ stats,
+                                                  const float* __restrict__ hub_adot,
+                                                  const int4* __restrict__ chunks,
+                                                  int64_t num_chunks, float slope,
+                                                  float* __restrict__ dpre,
+                                                  float* __restrict__ cpart) {
+  const int lane = threadIdx.x & 63, h = lane & 7;
+  const int64_t c = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  if (c >= num_chunks) return;
+  const int4 ck = uni4(chunks[c]);
+  const int64_t i = ck.w;
+  const float t_h = st[i * 16 + H + h];
+  const float m_h = stats[i * 16 + h];
+  const float inv_h = 1.0f / (stats[i * 16 + H + h] + kSoftmaxEps);
+  const float d = bwd_pass2(col, ck.y, ck.z, st, t_h, m_h, inv_h, hub_adot[int64_t(ck.x) * 8 + h],
+                            slope, dpre);
+  if (lane < 8) cpart[c * 8 + lane] = d;
+}
+
+// Per hub (one wave): out[row] = sum over its chunks of cpart[c][0:8], in a
+// fixed order (lane-strided partials, then an xor tree); row = hub_dst[hub]
+// when hub_dst is given, else the hub index.
+__global__ void __launch_bounds__(256) k_sum8(const float* __restrict__ cpart,
+                                              const int32_t* __restrict__ chunk_ptr,
+                                              int64_t num_hubs, const int32_t* __restrict__ hub_dst,
+                                              float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, h = lane & 7, k = lane >> 3;
+  const int64_t hb = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  if (hb >= num_hubs) return;
+  float s = 0.f;
+  for (int c = chunk_ptr[hb] + k; c < chunk_ptr[hb + 1]; c += 8) s += cpart[int64_t(c) * 8 + h];
+  s = sum_xor8_16_32(s);
+  if (lane < 8) out[(hub_dst ? int64_t(hub_dst[hb]) : hb) * 8 + lane] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Source side (CSC).  y_h = sum alpha~ g_i (lane = channel), ds = sum dpre
+// (head lane & 7, partial over the lane's messages).
+__device__ __forceinline__ void src_segment(const int32_t* __restrict__ csc_dst,
+                                            const int32_t* __restrict__ csc_eid, int p0, int p1,
+                                            const float* __restrict__ alpha_d,
+                                            const float* __restrict__ dpre,
+                                            const float* __restrict__ g, float (&y)[H],
+                                            float& ds) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  for (int b = p0; b < p1; b += 8) {
+    const int p = b + kk;
+    const bool valid = p < p1;
+    const int pc = valid ? p : p1 - 1;
+    const int e = csc_eid[pc];
+    const int i = csc_dst[pc];
+    const float a = valid ? alpha_d[int64_t(e) * 8 + h] : 0.f;
+    ds += valid ? dpre[int64_t(e) * 8 + h] : 0.f;
+    const int nk = min(8, p1 - b);
+    float gv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] = g[int64_t(__builtin_amdgcn_readlane(i, 8 * k)) * C + lane];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < nk) {
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh)
+          y[hh] = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), 8 * k + hh)),
+                       gv[k], y[hh]);
+      }
+    }
+  }
+}
+
+// dh' row j from y (lane = channel), ds (head lane & 7, complete) and dt_j
+__device__ __forceinline__ void write_dh(int64_t j, const float (&y)[H], float ds,
+                                         const float* __restrict__ dt,
+                                         const float* __restrict__ att_src,
+                                         const float* __restrict__ att_dst,
+                                         float* __restrict__ dh) {
+  const int lane = threadIdx.x & 63;
+  float* r = dh + j * kDH;
+  const float dtl = dt[j * 8 + (lane & 7)];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    const float dsh = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ds), hh));
+    const float dth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dtl), hh));
+    r[hh * C + lane] = fmaf(dth, att_dst[hh * C + lane],
+                            fmaf(dsh, att_src[hh * C + lane], y[hh] * (1.0f / H)));
+  }
+  if (lane < 8) {
+    r[HC + lane] = ds;
+    r[HC + H + lane] = dtl;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_bwd_src(
+    const int32_t* __restrict__ colptr, const int32_t* __restrict__ csc_dst,
+    const int32_t* __restrict__ csc_eid, int64_t N, const int32_t* __restrict__ src_hub_rank,
+    const float* __restrict__ alpha_d, const float* __restrict__ dpre,
+    const float* __restrict__ dt, const float* __restrict__ g, const float* __restrict__ att_src,
+    const float* __restrict__ att_dst, float* __restrict__ dh) {
+  const int64_t w0 = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t j = w0; j < N; j += nw) {
+    if (src_hub_rank && src_hub_rank[j] >= 0) continue;  // k_bwd_src_hub
+    float y[H];
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) y[hh] = 0.f;
+    float ds = 0.f;
+    src_segment(csc_dst, csc_eid, colptr[j], colptr[j + 1], alpha_d, dpre, g, y, ds);
+    write_dh(j, y, sum_xor8_16_32(ds), dt, att_src, att_dst, dh);
+  }
+}
+
+// source hub chunks {hub, p0, p1, src}: partial y (512) | ds (8) per chunk
+__global__ void __launch_bounds__(256) k_bwd_src_hub1(
+    const int32_t* __restrict__ csc_dst, const int32_t* __restrict__ csc_eid,
+    const int4* __restrict__ chunks, int64_t num_chunks, const float* __restrict__ alpha_d,
+    const float* __restrict__ dpre, const float* __restrict__ g, float* __restrict__ spart) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
+  if (c >= num_chunks) return;
+  const int4 ck = uni4(chunks[c]);
+  float y[H];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) y[hh] = 0.f;
+  float ds = 0.f;
+  src_segment(csc_dst, csc_eid, ck.y, ck.z, alpha_d, dpre, g, y, ds);
+  ds = sum_xor8_16_32(ds);
+  float* r = spart + c * (HC + H);
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) r[hh * C + lane] = y[hh];
+  if (lane < 8) r[HC + lane] = ds;
+}
+
+// one block (8 waves) per source hub: wave hh sums head hh's y over the chunks
+// in order; wave 0 also sums ds.  Then the dh' row.
+__global__ void __launch_bounds__(512) k_bwd_src_hub2(
+    const float* __restrict__ spart, const int32_t* __restrict__ chunk_ptr,
+    const int32_t* __restrict__ hub_src, const float* __restrict__ dt,
+    const float* __restrict__ att_src, const float* __restrict__ att_dst,
+    float* __restrict__ dh) {
+  const int lane = threadIdx.x & 63, hh = threadIdx.x >> 6;
+  const int64_t hb = blockIdx.x;
+  const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
+  float y = 0.f, ds = 0.f;
+  for (int c = c0; c < c1; ++c) {
+    const float* r = spart + int64_t(c) * (HC + H);
+    y += r[hh * C + lane];
+    if (hh == 0 && lane < 8) ds += r[HC + lane];
+  }
+  const int64_t j = hub_src[hb];
+  float* r = dh + j * kDH;
+  __shared__ float sds[8];  // wave 0's ds, for every head's wave
+  if (hh == 0 && lane < 8) sds[lane] = ds;
+  __syncthreads();
+  const float dth = dt[j * 8 + hh];
+  r[hh * C + lane] = fmaf(dth, att_dst[hh * C + lane],
+                          fmaf(sds[hh], att_src[hh * C + lane], y * (1.0f / H)));
+  if (hh == 0 && lane < 8) {
+    r[HC + lane] = sds[lane];
+    r[HC + H + lane] = dt[j * 8 + lane];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// grad_W' slabs: C_z[m][n] = sum_{k in split z} A[k][m] B[k][n] (both operands
+// k-major: A = dh' rows, B = x rows), fp32 MFMA 16x16x4.  Block tile 176 x 176
+// (11 waves, one 16-row strip each), BK = 16; m, n padded with zeros.
+constexpr int TT = 176, TK = 16, TW = 11;
+
+template <typename TB>
+__global__ void __launch_bounds__(TW * 64) k_gemm_tn(const float* __restrict__ A, int64_t lda,
+                                                     const TB* __restrict__ B, int64_t ldb,
+                                                     int64_t M, int64_t N, int64_t K,
+                                                     int64_t k_per_split,
+                                                     float* __restrict__ slab) {
+  __shared__ float As[TK][TT + 4];
+  __shared__ float Bs[TK][TT + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = int64_t(blockIdx.x) * TT, n0 = int64_t(blockIdx.y) * TT;
+  const int64_t kb = int64_t(blockIdx.z) * k_per_split;
+  const int64_t ke = min(K, kb + k_per_split);
+  f32x4 acc[TT / 16];
+#pragma unroll
+  for (int t = 0; t < TT / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t k0 = kb; k0 < ke; k0 += TK) {
+    for (int idx = tid; idx < TK * TT; idx += TW * 64) {
+      const int kk = idx / TT, mm = idx - kk * TT;
+      const int64_t gk = k0 + kk;
+      const bool kin = gk < ke;
+      As[kk][mm] = (kin && m0 + mm < M) ? A[gk * lda + m0 + mm] : 0.f;
+      Bs[kk][mm] = (kin && n0 + mm < N) ? ldx1(B + gk * ldb + n0 + mm) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 4) {
+      const float a = As[kk + (lane >> 4)][wave * 16 + (lane & 15)];
+#pragma unroll
+      for (int t = 0; t < TT / 16; ++t) {
+        const float b = Bs[kk + (lane >> 4)][t * 16 + (lane & 15)];
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  float* Cz = slab + int64_t(blockIdx.z) * M * N;
+#pragma unroll
+  for (int t = 0; t < TT / 16; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t gm = m0 + wave * 16 + (lane >> 4) * 4 + r;
+      const int64_t gn = n0 + t * 16 + (lane & 15);
+      if (gm < M && gn < N) Cz[gm * N + gn] = acc[t][r];
+    }
+}
+
+// Generic strided GEMM (grad_x = dh W): Cm(m, n) = sum_k A(m, k) B(k, n),
+// X(r, c) = X[r * s_r + c * s_c]; 64x64 tile, BK = 16, 4 waves of 32x32.
 constexpr int GB = 64, GK = 16;
 
 __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int64_t sam,
                                               int64_t sak, const float* __restrict__ B,
                                               int64_t sbk, int64_t sbn, float* __restrict__ Cm,
-                                              int64_t scm, int64_t scn, int64_t M, int64_t N,
-                                              int64_t K, int64_t k_per_split) {
+                                              int64_t scm, int64_t M, int64_t N, int64_t K) {
   __shared__ float As[GK][GB + 4];
   __shared__ float Bs[GK][GB + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t m0 = int64_t(blockIdx.x) * GB, n0 = int64_t(blockIdx.y) * GB;
-  const int64_t kb = int64_t(blockIdx.z) * k_per_split;
-  const int64_t ke = min(K, kb + k_per_split);
   const int wm = wave >> 1, wn = wave & 1;
   f32x4 acc[2][2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t k0 = kb; k0 < ke; k0 += GK) {
+    for (int v = 0; v < 2; ++v) acc[t][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t k0 = 0; k0 < K; k0 += GK) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int idx = tid + 256 * q;  // 0..1023 = GK x GB
-      // A tile: element (m = idx % GB, k = idx / GB)  [contiguous m when sam==1]
-      // choose the mapping that keeps the unit-stride index in the lane
+      const int idx = tid + 256 * q;
       int mm, kk;
       if (sak == 1) { kk = idx % GK; mm = idx / GK; } else { mm = idx % GB; kk = idx / GB; }
       const int64_t gm = m0 + mm, gk = k0 + kk;
-      As[kk][mm] = (gm < M && gk < ke) ? A[gm * sam + gk * sak] : 0.f;
+      As[kk][mm] = (gm < M && gk < K) ? A[gm * sam + gk * sak] : 0.f;
       int nn, kq;
       if (sbk == 1) { kq = idx % GK; nn = idx / GK; } else { nn = idx % GB; kq = idx / GB; }
       const int64_t gn = n0 + nn, gk2 = k0 + kq;
-      Bs[kq][nn] = (gn < N && gk2 < ke) ? B[gk2 * sbk + gn * sbn] : 0.f;
+      Bs[kq][nn] = (gn < N && gk2 < K) ? B[gk2 * sbk + gn * sbn] : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -65,264 +619,302 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int64
 #pragma unroll
       for (int t = 0; t < 2; ++t) a[t] = As[kk + (lane >> 4)][wm * 32 + t * 16 + (lane & 15)];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) b[u] = Bs[kk + (lane >> 4)][wn * 32 + u * 16 + (lane & 15)];
+      for (int v = 0; v < 2; ++v) b[v] = Bs[kk + (lane >> 4)][wn * 32 + v * 16 + (lane & 15)];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[u], acc[t][u], 0, 0, 0);
+        for (int v = 0; v < 2; ++v)
+          acc[t][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[v], acc[t][v], 0, 0, 0);
     }
     __syncthreads();
   }
-  const bool atomic = gridDim.z > 1;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int v = 0; v < 2; ++v)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t gm = m0 + wm * 32 + t * 16 + (lane >> 4) * 4 + r;
-        const int64_t gn = n0 + wn * 32 + u * 16 + (lane & 15);
-        if (gm < M && gn < N) {
-          float* p = Cm + gm * scm + gn * scn;
-          if (atomic) atomicAdd(p, acc[t][u][r]);
-          else *p = acc[t][u][r];
-        }
+        const int64_t gn = n0 + wn * 32 + v * 16 + (lane & 15);
+        if (gm < M && gn < N) Cm[gm * scm + gn] = acc[t][v][r];
       }
 }
 
-gfd_status gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
-                float* Cm, int64_t scm, int64_t scn, int64_t M, int64_t N, int64_t K, int splits,
-                hipStream_t stream) {
-  if (M <= 0 || N <= 0) return GFD_OK;
-  int64_t kps = (K + splits - 1) / splits;
-  kps = (kps + GK - 1) / GK * GK;
-  if (kps <= 0) kps = GK;
-  int64_t z = (K + kps - 1) / kps;
-  if (z < 1) z = 1;
-  dim3 grid(unsigned((M + GB - 1) / GB), unsigned((N + GB - 1) / GB), unsigned(z));
-  k_gemm<<<grid, 256, 0, stream>>>(A, sam, sak, B, sbk, sbn, Cm, scm, scn, M, N, K, kps);
+// out[c * so] = sum_{r < rows} part[r * ld + c], r ascending (a fixed order)
+__global__ void __launch_bounds__(256) k_reduce_rows(const float* __restrict__ part, int64_t rows,
+                                                     int64_t ld, int64_t cols,
+                                                     float* __restrict__ out, int64_t so) {
+  for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c < cols;
+       c += int64_t(gridDim.x) * blockDim.x) {
+    float s = 0.f;
+    for (int64_t r = 0; r < rows; ++r) s += part[r * ld + c];
+    out[c * so] = s;
+  }
+}
+
+// column sums of a [n, 64] fp32 matrix: fixed-grid partials part[block][64]
+__global__ void __launch_bounds__(256) k_colsum64(const float* __restrict__ a, int64_t n,
+                                                  float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float s = 0.f;
+  for (int64_t r = int64_t(blockIdx.x) * 4 + w; r < n; r += int64_t(gridDim.x) * 4)
+    s += a[r * C + lane];
+  red[w][lane] = s;
+  __syncthreads();
+  if (threadIdx.x < 64)
+    part[int64_t(blockIdx.x) * 64 + lane] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// grad_att_src[h][c] = sum_f W[h C + c][f] S_h[f] (rows HC.. of gw'), att_dst from T
+__global__ void __launch_bounds__(256) k_att_grad(const float* __restrict__ W, int F,
+                                                  const float* __restrict__ gw,
+                                                  float* __restrict__ gas, float* __restrict__ gad) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;  // 0 .. 2 HC
+  if (o >= 2 * HC) return;
+  const int which = o / HC, hc = o - which * HC, h = hc / C;
+  const float* w = W + int64_t(hc) * F;
+  const float* s = gw + int64_t(HC + which * H + h) * F;
+  float acc = 0.f;
+  for (int f = 0; f < F; ++f) acc = fmaf(w[f], s[f], acc);
+  (which ? gad : gas)[hc] = acc;
+}
+
+int wsplits(int64_t N) {
+  int64_t s = N / 8192;
+  if (s < 1) s = 1;
+  if (s > 512) s = 512;
+  return int(s);
+}
+
+int kf_fu(int F) { return (F + 63) / 64; }
+
+struct BwdLayout {
+  size_t whdr, bhi, blo, dpre, alpha, dt, uhub, cpart, hadot, spart, dh, slab, gw, gbp;
+};
+
+BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
+                     int64_t src_chunks, Sizer& s) {
+  BwdLayout L;
+  const int Fu = (F + 15) / 16 * 16;
+  const int NT = Fu / 16;
+  const int64_t ch = chunks > 0 ? chunks : 0;
+  auto take = [&](size_t bytes) { size_t o = align_up(s.off, 256); s.off = o + bytes; return o; };
+  L.whdr = take(64);
+  L.bhi = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
+  L.blo = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
+  L.dpre = take(sizeof(float) * size_t(M) * 8);
+  L.alpha = take(sizeof(float) * size_t(M) * 8);
+  L.dt = take(sizeof(float) * size_t(N) * 8);
+  L.uhub = take(sizeof(float) * size_t(hubs > 0 ? hubs : 0) * H * Fu);
+  L.cpart = take(sizeof(float) * size_t(ch) * 8);
+  L.hadot = take(sizeof(float) * size_t(hubs > 0 ? hubs : 0) * 8);
+  L.spart = take(sizeof(float) * size_t(src_chunks > 0 ? src_chunks : 0) * (HC + H));
+  L.dh = take(sizeof(float) * size_t(N) * kDH);
+  L.slab = take(sizeof(float) * size_t(wsplits(N)) * kDH * F);
+  L.gw = take(sizeof(float) * size_t(kDH) * F);
+  L.gbp = take(sizeof(float) * size_t(kRedBlocks) * 64);
+  return L;
+}
+
+template <typename XT, int KF>
+gfd_status launch_msg(const void* x, int F, int Fu, int64_t ldx, const int32_t* rowptr,
+                      const int32_t* col, int64_t N, const gfd_plan* plan, const float* st,
+                      const float* stats, const float* g, const float* whdr, const uint4* bhi,
+                      const uint4* blo, float slope, float dp, uint64_t seed, float* uhub,
+                      float* dpre, float* alpha_d, float* dt, float* cpart, float* hadot,
+                      hipStream_t stream) {
+  const size_t smem = msg_smem(Fu);
+  if (!ensure_lds(reinterpret_cast<const void*>(&k_bwd_msg<XT, KF>), smem))
+    return GFD_ERR_HIP;
+  const int64_t tiles = (N + kUT - 1) / kUT;
+  const bool hubs = plan && plan->num_hubs > 0;
+  k_bwd_msg<XT, KF><<<unsigned(tiles), kUW * 64, smem, stream>>>(
+      x, F, Fu, ldx, rowptr, col, N,
+      plan ? reinterpret_cast<const int4*>(plan->slot_desc) : nullptr,
+      hubs ? plan->hub_rank : nullptr, st, stats, g, whdr, bhi, blo, slope, dp, seed, uhub, dpre,
+      alpha_d, dt);
+  GFD_LAUNCH_CHECK();
+  if (!hubs) return GFD_OK;
+  const int64_t nc = plan->num_chunks, nh = plan->num_hubs;
+  const int4* chunks = reinterpret_cast<const int4*>(plan->hub_chunk);
+  k_bwd_hub1<XT, KF><<<unsigned((nc + 3) / 4), 256, 0, stream>>>(
+      x, F, Fu, ldx, col, st, stats, uhub, chunks, nc, slope, dp, seed, dpre, alpha_d, cpart);
+  GFD_LAUNCH_CHECK();
+  k_sum8<<<unsigned((nh + 3) / 4), 256, 0, stream>>>(cpart, plan->hub_chunk_ptr, nh, nullptr,
+                                                     hadot);
+  GFD_LAUNCH_CHECK();
+  k_bwd_hub2<<<unsigned((nc + 3) / 4), 256, 0, stream>>>(col, st, stats, hadot, chunks, nc, slope,
+                                                         dpre, cpart);
+  GFD_LAUNCH_CHECK();
+  k_sum8<<<unsigned((nh + 3) / 4), 256, 0, stream>>>(cpart, plan->hub_chunk_ptr, nh,
+                                                     plan->hub_dst, dt);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
 
-// ---------------------------------------------------------------------------
-// dst-centric backward.  Lane layout for logits: lane = 8k + h.
-__global__ void __launch_bounds__(256) k_bwd_dst(
-    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, int64_t N,
-    const float* __restrict__ st, const float* __restrict__ stats, const float* __restrict__ hproj,
-    const float* __restrict__ g, float slope, float dp, uint64_t seed, float* __restrict__ dpre,
-    float* __restrict__ alpha_d, float* __restrict__ dt, float* __restrict__ grad_bias) {
-  const int lane = threadIdx.x & 63;
-  const int h = lane & 7, kk = lane >> 3;
-  const int64_t w0 = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
-  const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  const float keep_scale = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
-  float gb = 0.f;
-  for (int64_t i = w0; i < N; i += nw) {
-    const int e0 = rowptr[i], e1 = rowptr[i + 1];
-    const float gc = g[i * C + lane];  // lane = channel
-    gb += gc;
-    const float t_h = st[i * 16 + H + h];
-    const float m_h = stats[i * 16 + h];
-    const float inv_h = 1.0f / (stats[i * 16 + H + h] + kSoftmaxEps);
-    // pass 1: alpha, dA (grad wrt pre-dropout alpha), sum alpha*dA
-    float adot = 0.f;
-    for (int b = e0; b < e1; b += 8) {
-      const int e = b + kk;
-      float al = 0.f, keepf = 0.f;
-      int j = 0;
-      if (e < e1) {
-        j = col[e];
-        al = __expf(leaky(st[int64_t(j) * 16 + h] + t_h, slope) - m_h) * inv_h;
-        keepf = (dp > 0.f) ? (dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? keep_scale : 0.f)
-                           : 1.0f;
-      }
-      float my_da = 0.f;
-      const int nk = min(8, e1 - b);
-      for (int k = 0; k < nk; ++k) {
-        const int jk = __builtin_amdgcn_readlane(j, 8 * k);
-        const float* hr = hproj + int64_t(jk) * HC;
-        float v[H];
-#pragma unroll
-        for (int hh = 0; hh < H; ++hh) v[hh] = gc * hr[hh * C + lane];
-        // transposing reduce over 64 lanes: lane ends with head (lane >> 3)
-#pragma unroll
-        for (int step = 0; step < 3; ++step) {
-          const int half = 4 >> step;
-          const int mask = 32 >> step;
-          const bool up = (lane & mask) != 0;
-#pragma unroll
-          for (int q = 0; q < half; ++q) {
-            float send = up ? v[q] : v[q + half];
-            float keep = up ? v[q + half] : v[q];
-            v[q] = keep + __shfl_xor(send, mask);
-          }
-        }
-        float r = v[0];
-        r += __shfl_xor(r, 4);
-        r += __shfl_xor(r, 2);
-        r += __shfl_xor(r, 1);
-        // lane 8k+h needs head h of edge k: lives in lanes 8h..8h+7
-        const float got = __shfl(r, 8 * h);
-        if (kk == k) my_da = got;
-      }
-      if (e < e1) {
-        const float da = my_da * (1.0f / H) * keepf;  // d alpha (pre-dropout)
-        adot = fmaf(al, da, adot);
-        dpre[int64_t(e) * 8 + h] = da;                // stash, finished in pass 2
-        alpha_d[int64_t(e) * 8 + h] = al * keepf;
-      }
-    }
-    adot += __shfl_xor(adot, 8);
-    adot += __shfl_xor(adot, 16);
-    adot += __shfl_xor(adot, 32);
-    // pass 2: de = alpha (dA - sum); dpre = de * leaky'(pre); dt_i = sum dpre
-    float dts = 0.f;
-    for (int b = e0; b < e1; b += 8) {
-      const int e = b + kk;
-      if (e < e1) {
-        const int j = col[e];
-        const float pre = st[int64_t(j) * 16 + h] + t_h;
-        const float al = __expf(leaky(pre, slope) - m_h) * inv_h;
-        const float da = dpre[int64_t(e) * 8 + h];
-        const float d = al * (da - adot) * (pre > 0.f ? 1.0f : slope);
-        dpre[int64_t(e) * 8 + h] = d;
-        dts += d;
-      }
-    }
-    dts += __shfl_xor(dts, 8);
-    dts += __shfl_xor(dts, 16);
-    dts += __shfl_xor(dts, 32);
-    if (lane < 8) dt[i * 8 + lane] = dts;
+template <typename XT>
+gfd_status launch_msg_x(int KF, const void* x, int F, int Fu, int64_t ldx, const int32_t* rowptr,
+                        const int32_t* col, int64_t N, const gfd_plan* plan, const float* st,
+                        const float* stats, const float* g, const float* whdr, const uint4* bhi,
+                        const uint4* blo, float slope, float dp, uint64_t seed, float* uhub,
+                        float* dpre, float* alpha_d, float* dt, float* cpart, float* hadot,
+                        hipStream_t stream) {
+#define GFD_MSG(K)                                                                            \
+  return launch_msg<XT, K>(x, F, Fu, ldx, rowptr, col, N, plan, st, stats, g, whdr, bhi, blo, \
+                           slope, dp, seed, uhub, dpre, alpha_d, dt, cpart, hadot, stream)
+  switch (KF) {
+    case 1: GFD_MSG(1);
+    case 2: GFD_MSG(2);
+    case 3: GFD_MSG(3);
+    case 4: GFD_MSG(4);
+    default: return GFD_ERR_UNSUPPORTED;
   }
-  if (grad_bias) atomicAdd(&grad_bias[lane], gb);
+#undef GFD_MSG
 }
 
-// src-centric: one wave per source node j; lane = channel c.
-__global__ void __launch_bounds__(256) k_bwd_src(
-    const int32_t* __restrict__ colptr, const int32_t* __restrict__ csc_dst,
-    const int32_t* __restrict__ csc_eid, int64_t N, const float* __restrict__ dpre,
-    const float* __restrict__ alpha_d, const float* __restrict__ dt, const float* __restrict__ g,
-    const float* __restrict__ hproj, const float* __restrict__ att_src,
-    const float* __restrict__ att_dst, float* __restrict__ dh, float* __restrict__ grad_as,
-    float* __restrict__ grad_ad) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w0 = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
-  const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  float as[H], ad[H], gas[H], gad[H];
-#pragma unroll
-  for (int hh = 0; hh < H; ++hh) {
-    as[hh] = att_src[hh * C + lane];
-    ad[hh] = att_dst[hh * C + lane];
-    gas[hh] = 0.f;
-    gad[hh] = 0.f;
-  }
-  for (int64_t j = w0; j < N; j += nw) {
-    const int p0 = colptr[j], p1 = colptr[j + 1];
-    float y[H], ds[H];
-#pragma unroll
-    for (int hh = 0; hh < H; ++hh) { y[hh] = 0.f; ds[hh] = 0.f; }
-    for (int p = p0; p < p1; ++p) {
-      const int e = csc_eid[p];
-      const int i = csc_dst[p];
-      const float gi = g[int64_t(i) * C + lane];
-#pragma unroll
-      for (int hh = 0; hh < H; ++hh) {
-        y[hh] = fmaf(alpha_d[int64_t(e) * 8 + hh], gi, y[hh]);
-        ds[hh] += dpre[int64_t(e) * 8 + hh];
-      }
-    }
-    const float* hr = hproj + j * HC;
-    float* dr = dh + j * HC;
-#pragma unroll
-    for (int hh = 0; hh < H; ++hh) {
-      const float dtv = dt[j * 8 + hh];
-      dr[hh * C + lane] = y[hh] * (1.0f / H) + ds[hh] * as[hh] + dtv * ad[hh];
-      const float hv = hr[hh * C + lane];
-      gas[hh] = fmaf(ds[hh], hv, gas[hh]);
-      gad[hh] = fmaf(dtv, hv, gad[hh]);
-    }
-  }
-#pragma unroll
-  for (int hh = 0; hh < H; ++hh) {
-    atomicAdd(&grad_as[hh * C + lane], gas[hh]);
-    atomicAdd(&grad_ad[hh * C + lane], gad[hh]);
-  }
-}
+template <typename XT>
+gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
+                    const int32_t* col, const gfd_plan* plan, const int32_t* colptr,
+                    const int32_t* csc_dst, const int32_t* csc_eid, const gfd_plan* src_plan,
+                    int64_t M, const float* W, const float* att_src, const float* att_dst,
+                    float slope, float dp, uint64_t seed, const float* st, const float* stats,
+                    const float* g, float* grad_x, float* grad_W, float* grad_as, float* grad_ad,
+                    float* grad_bias, void* ws, hipStream_t stream) {
+  const int64_t hubs = plan ? plan->num_hubs : 0, chunks = plan ? plan->num_chunks : 0;
+  const int64_t shubs = src_plan ? src_plan->num_hubs : 0;
+  const int64_t schunks = src_plan ? src_plan->num_chunks : 0;
+  Sizer sz;
+  const BwdLayout L = bwd_layout(N, M, F, hubs, chunks, schunks, sz);
+  char* b = static_cast<char*>(ws);
+  float* whdr = reinterpret_cast<float*>(b + L.whdr);
+  uint4* bhi = reinterpret_cast<uint4*>(b + L.bhi);
+  uint4* blo = reinterpret_cast<uint4*>(b + L.blo);
+  float* dpre = reinterpret_cast<float*>(b + L.dpre);
+  float* alpha_d = reinterpret_cast<float*>(b + L.alpha);
+  float* dt = reinterpret_cast<float*>(b + L.dt);
+  float* uhub = reinterpret_cast<float*>(b + L.uhub);
+  float* cpart = reinterpret_cast<float*>(b + L.cpart);
+  float* hadot = reinterpret_cast<float*>(b + L.hadot);
+  float* spart = reinterpret_cast<float*>(b + L.spart);
+  float* dh = reinterpret_cast<float*>(b + L.dh);
+  float* slab = reinterpret_cast<float*>(b + L.slab);
+  float* gw = reinterpret_cast<float*>(b + L.gw);
+  float* gbp = reinterpret_cast<float*>(b + L.gbp);
+  const int Fu = (F + 15) / 16 * 16, NT = Fu / 16;
+  gfd_status s;
 
-int waves_grid(int64_t n) {
-  int64_t blocks = (n + 3) / 4;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  return int(blocks);
+  // 1. W fragments for U = G W
+  k_bwd_wmax<<<1, 1024, 0, stream>>>(W, HC * F, whdr);
+  GFD_LAUNCH_CHECK();
+  const int64_t nfr = int64_t(H) * 2 * NT * 64;
+  k_bwd_wpack<<<unsigned((nfr + 255) / 256), 256, 0, stream>>>(W, F, NT, whdr, bhi, blo);
+  GFD_LAUNCH_CHECK();
+  // 2. destination side: dA, alpha~, softmax backward, dt
+  s = launch_msg_x<XT>(kf_fu(F), x, F, Fu, ldx, rowptr, col, N, plan, st, stats, g, whdr, bhi,
+                       blo, slope, dp, seed, uhub, dpre, alpha_d, dt, cpart, hadot, stream);
+  if (s != GFD_OK) return s;
+  // 3. source side: dh' rows
+  {
+    int64_t blocks = (N + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
+    k_bwd_src<<<unsigned(blocks), 256, 0, stream>>>(colptr, csc_dst, csc_eid, N,
+                                                    shubs > 0 ? src_plan->hub_rank : nullptr,
+                                                    alpha_d, dpre, dt, g, att_src, att_dst, dh);
+    GFD_LAUNCH_CHECK();
+    if (shubs > 0) {
+      k_bwd_src_hub1<<<unsigned((schunks + 3) / 4), 256, 0, stream>>>(
+          csc_dst, csc_eid, reinterpret_cast<const int4*>(src_plan->hub_chunk), schunks, alpha_d,
+          dpre, g, spart);
+      GFD_LAUNCH_CHECK();
+      k_bwd_src_hub2<<<unsigned(shubs), 512, 0, stream>>>(spart, src_plan->hub_chunk_ptr,
+                                                          src_plan->hub_dst, dt, att_src, att_dst,
+                                                          dh);
+      GFD_LAUNCH_CHECK();
+    }
+  }
+  // 4. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
+  {
+    const int splits = wsplits(N);
+    int64_t kps = (N + splits - 1) / splits;
+    kps = (kps + TK - 1) / TK * TK;
+    const int64_t z = (N + kps - 1) / kps;
+    dim3 grid(unsigned((kDH + TT - 1) / TT), unsigned((F + TT - 1) / TT), unsigned(z));
+    k_gemm_tn<typename XT::T><<<grid, TW * 64, 0, stream>>>(dh, kDH, x, ldx, kDH, F, N, kps, slab);
+    GFD_LAUNCH_CHECK();
+    const int64_t cols = int64_t(kDH) * F;
+    k_reduce_rows<<<unsigned((cols + 255) / 256), 256, 0, stream>>>(slab, z, cols, cols, gw, 1);
+    GFD_LAUNCH_CHECK();
+    GFD_HIP_CHECK(hipMemcpyAsync(grad_W, gw, sizeof(float) * HC * F, hipMemcpyDeviceToDevice,
+                                 stream));
+    k_att_grad<<<(2 * HC + 255) / 256, 256, 0, stream>>>(W, F, gw, grad_as, grad_ad);
+    GFD_LAUNCH_CHECK();
+  }
+  // 5. grad_bias = sum_i g_i
+  if (grad_bias) {
+    k_colsum64<<<kRedBlocks, 256, 0, stream>>>(g, N, gbp);
+    GFD_LAUNCH_CHECK();
+    k_reduce_rows<<<1, 64, 0, stream>>>(gbp, kRedBlocks, 64, 64, grad_bias, 1);
+    GFD_LAUNCH_CHECK();
+  }
+  // 6. grad_x = dh W  (A = dh [N, 512] at row stride 528, B = W [512, F])
+  if (grad_x) {
+    dim3 grid(unsigned((N + GB - 1) / GB), unsigned((F + GB - 1) / GB));
+    k_gemm<<<grid, 256, 0, stream>>>(dh, kDH, 1, W, F, 1, grad_x, F, N, F, HC);
+    GFD_LAUNCH_CHECK();
+  }
+  return GFD_OK;
 }
 
 }  // namespace
 
 extern "C" {
 
-size_t gfd_gat_bwd_workspace_size(int64_t N, int64_t M, int F, int heads, int channels) {
+size_t gfd_gat_bwd_workspace_size(int64_t N, int64_t M, int F, int heads, int channels,
+                                  int64_t num_hubs, int64_t num_chunks, int64_t src_chunks) {
   if (heads != H || channels != C || F < 1 || F > 256 || N <= 0 || M < 0) return 0;
   Sizer s;
-  s.take<float>(size_t(N) * HC);  // h
-  s.take<float>(size_t(N) * HC);  // dh
-  s.take<float>(size_t(M) * 8);   // dpre
-  s.take<float>(size_t(M) * 8);   // alpha_d
-  s.take<float>(size_t(N) * 8);   // dt
+  bwd_layout(N, M, F, num_hubs, num_chunks, src_chunks, s);
   return s.off;
 }
 
 gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
-                       const int32_t* rowptr,
-                       const int32_t* col, const int32_t* colptr, const int32_t* csc_dst,
-                       const int32_t* csc_eid, int64_t M, const float* W, const float* att_src,
+                       const int32_t* rowptr, const int32_t* col, const gfd_plan* plan,
+                       const int32_t* colptr, const int32_t* csc_dst, const int32_t* csc_eid,
+                       const gfd_plan* src_plan, int64_t M, const float* W, const float* att_src,
                        const float* att_dst, int heads, int channels, float slope, float dp,
                        uint64_t seed, const float* st, const float* stats, const float* g,
                        float* grad_x, float* grad_W, float* grad_as, float* grad_ad,
                        float* grad_bias, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (heads != H || channels != C || F < 1 || F > 256) return GFD_ERR_UNSUPPORTED;
-  if (x_dtype != GFD_DTYPE_F32) return x_dtype == GFD_DTYPE_BF16 ? GFD_ERR_UNSUPPORTED : GFD_ERR_ARGUMENT;
-  const float* x = static_cast<const float*>(xv);
-  if (N <= 0 || M <= 0 || !x || !rowptr || !col || !colptr || !csc_dst || !csc_eid || !W ||
-      !att_src || !att_dst || !st || !stats || !g || !grad_W || !grad_as || !grad_ad || ldx < F)
+  if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
+  if (N <= 0 || M <= 0 || !xv || !rowptr || !col || !colptr || !csc_dst || !csc_eid || !W ||
+      !att_src || !att_dst || !st || !stats || !g || !grad_W || !grad_as || !grad_ad || !ws ||
+      ldx < F)
     return GFD_ERR_ARGUMENT;
   if (!(dp >= 0.f && dp < 1.f)) return GFD_ERR_ARGUMENT;
-  if (ws_bytes < gfd_gat_bwd_workspace_size(N, M, F, heads, channels)) return GFD_ERR_WORKSPACE;
-  Carve c(ws, ws_bytes);
-  float* hproj = c.take<float>(size_t(N) * HC);
-  float* dh = c.take<float>(size_t(N) * HC);
-  float* dpre = c.take<float>(size_t(M) * 8);
-  float* alpha_d = c.take<float>(size_t(M) * 8);
-  float* dt = c.take<float>(size_t(N) * 8);
-  if (!c.ok) return GFD_ERR_WORKSPACE;
-
-  // h = x W^T  (A = x [N,F], B(k=f, n) = W[n][f])
-  gfd_status s = gemm(x, ldx, 1, W, 1, F, hproj, HC, 1, N, HC, F, 1, stream);
-  if (s != GFD_OK) return s;
-  GFD_HIP_CHECK(hipMemsetAsync(grad_as, 0, sizeof(float) * HC, stream));
-  GFD_HIP_CHECK(hipMemsetAsync(grad_ad, 0, sizeof(float) * HC, stream));
-  if (grad_bias) GFD_HIP_CHECK(hipMemsetAsync(grad_bias, 0, sizeof(float) * C, stream));
-  k_bwd_dst<<<waves_grid(N), 256, 0, stream>>>(rowptr, col, N, st, stats, hproj, g, slope, dp,
-                                               seed, dpre, alpha_d, dt, grad_bias);
-  GFD_LAUNCH_CHECK();
-  k_bwd_src<<<waves_grid(N), 256, 0, stream>>>(colptr, csc_dst, csc_eid, N, dpre, alpha_d, dt, g,
-                                               hproj, att_src, att_dst, dh, grad_as, grad_ad);
-  GFD_LAUNCH_CHECK();
-  // grad_W = dh^T x : M=HC (A(m,k=i) = dh[i][m]), N=F, K=N nodes, split-K
-  GFD_HIP_CHECK(hipMemsetAsync(grad_W, 0, sizeof(float) * HC * F, stream));
-  int splits = int(N / 4096);
-  if (splits < 1) splits = 1;
-  if (splits > 256) splits = 256;
-  s = gemm(dh, 1, HC, x, ldx, 1, grad_W, F, 1, HC, F, N, splits, stream);
-  if (s != GFD_OK) return s;
-  if (grad_x) {
-    // grad_x = dh W : A = dh [N, HC], B(k, n=f) = W[k][f]
-    s = gemm(dh, HC, 1, W, F, 1, grad_x, F, 1, N, F, HC, 1, stream);
-    if (s != GFD_OK) return s;
-  }
-  return GFD_OK;
+  if (N > 0x7fffffff || M > 0x7fffffff || ldx * (x_dtype == GFD_DTYPE_BF16 ? 2 : 4) > 0xffffffffLL)
+    return GFD_ERR_UNSUPPORTED;
+  if (plan && plan->num_hubs > 0 && (!plan->hub_rank || !plan->hub_chunk || !plan->hub_chunk_ptr ||
+                                     !plan->hub_dst))
+    return GFD_ERR_ARGUMENT;
+  if (src_plan && src_plan->num_hubs > 0 &&
+      (!src_plan->hub_rank || !src_plan->hub_chunk || !src_plan->hub_chunk_ptr ||
+       !src_plan->hub_dst))
+    return GFD_ERR_ARGUMENT;
+  if (ws_bytes < gfd_gat_bwd_workspace_size(N, M, F, heads, channels,
+                                            plan ? plan->num_hubs : 0,
+                                            plan ? plan->num_chunks : 0,
+                                            src_plan ? src_plan->num_chunks : 0))
+    return GFD_ERR_WORKSPACE;
+  if (x_dtype == GFD_DTYPE_BF16)
+    return bwd_impl<XBF16>(static_cast<const uint16_t*>(xv), N, F, ldx, rowptr, col, plan, colptr,
+                    csc_dst, csc_eid, src_plan, M, W, att_src, att_dst, slope, dp, seed, st, stats,
+                    g, grad_x, grad_W, grad_as, grad_ad, grad_bias, ws, stream);
+  return bwd_impl<XF32>(static_cast<const float*>(xv), N, F, ldx, rowptr, col, plan, colptr, csc_dst,
+                  csc_eid, src_plan, M, W, att_src, att_dst, slope, dp, seed, st, stats, g, grad_x,
+                  grad_W, grad_as, grad_ad, grad_bias, ws, stream);
 }
 
 }  // extern "C"

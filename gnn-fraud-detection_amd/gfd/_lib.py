@@ -74,10 +74,11 @@ SIGNATURES = {
                                      ct.c_int, P, P, P, c_sz, P]),
     "gfd_gat_fwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,
                             ct.c_int, c_f32, c_f32, c_u64, PLAN, P, P, P, P, c_sz, P]),
-    "gfd_gat_bwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int]),
-    "gfd_gat_bwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, P,
-                            ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, P, P, P, P, P,
-                            c_sz, P]),
+    "gfd_gat_bwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int, c_i64,
+                                          c_i64, c_i64]),
+    "gfd_gat_bwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, PLAN, P, P, P, PLAN, c_i64,
+                            P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, P, P, P,
+                            P, P, c_sz, P]),
 }
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "edge index out of range", 3: "workspace too small",

@@ -30,6 +30,9 @@ from . import _lib
 
 HUB_THRESHOLD = int(os.environ.get("GFD_HUB_THRESHOLD", "128"))
 HUB_CHUNK = int(os.environ.get("GFD_HUB_CHUNK", "128"))
+# source hubs of the backward's CSC pass (k_bwd_src chunks)
+SRC_HUB_THRESHOLD = 512
+SRC_HUB_CHUNK = 512
 
 
 def _ws(nbytes: int, device) -> torch.Tensor:
@@ -94,19 +97,8 @@ def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THR
     dev = rowptr.device
     lib = _lib.load()
     stream = _lib.stream_handle(dev)
-    max_hubs = num_messages // (threshold + 1) + 1
-    max_chunks = num_messages // chunk + max_hubs + 1
-    hub_rank = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-    hub_chunk = torch.empty(4 * max_chunks, dtype=torch.int32, device=dev)
-    hub_chunk_ptr = torch.empty(max_hubs + 1, dtype=torch.int32, device=dev)
-    hub_dst = torch.empty(max_hubs, dtype=torch.int32, device=dev)
-    nh, nc = _lib.c_i64(0), _lib.c_i64(0)
-    if n > 0:
-        ws = _ws(lib.gfd_plan_workspace_size(n), dev)
-        _lib.call("gfd_plan_hubs", rowptr.data_ptr(), n, threshold, chunk, hub_rank.data_ptr(),
-                  hub_chunk.data_ptr(), hub_chunk_ptr.data_ptr(), hub_dst.data_ptr(), max_hubs,
-                  max_chunks, _lib.ct.byref(nh), _lib.ct.byref(nc), ws.data_ptr(), ws.numel(),
-                  stream)
+    hub_rank, hub_chunk, hub_chunk_ptr, hub_dst, nh, nc = _hubs(rowptr, num_messages, threshold,
+                                                                chunk)
     row_order = None
     if order and n > 0:
         row_order = torch.empty(n, dtype=torch.int32, device=dev)
@@ -121,11 +113,43 @@ def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THR
             slot_cols = torch.empty(8 * n, dtype=torch.int32, device=dev)
             class_split = torch.empty(2, dtype=torch.int64, device=dev)
         _lib.call("gfd_plan_desc", rowptr.data_ptr(), _lib.ptr(col), n, _lib.ptr(row_order),
-                  hub_rank.data_ptr() if nh.value > 0 else None, slot_desc.data_ptr(),
+                  hub_rank.data_ptr() if nh > 0 else None, slot_desc.data_ptr(),
                   _lib.ptr(slot_cols), _lib.ptr(class_split), stream)
-    return Plan(n, row_order, slot_desc, slot_cols, hub_rank, hub_chunk[:4 * nc.value],
-                hub_chunk_ptr[:nh.value + 1], hub_dst[:nh.value], nh.value, nc.value,
-                class_split)
+    return Plan(n, row_order, slot_desc, slot_cols, hub_rank, hub_chunk, hub_chunk_ptr, hub_dst,
+                nh, nc, class_split)
+
+
+def _hubs(rowptr: torch.Tensor, num_messages: int, threshold: int, chunk: int):
+    """gfd_plan_hubs: rows with more than ``threshold`` entries split into
+    chunks of at most ``chunk`` (one sync)."""
+    n = rowptr.numel() - 1
+    dev = rowptr.device
+    lib = _lib.load()
+    max_hubs = num_messages // (threshold + 1) + 1
+    max_chunks = num_messages // chunk + max_hubs + 1
+    hub_rank = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    hub_chunk = torch.empty(4 * max_chunks, dtype=torch.int32, device=dev)
+    hub_chunk_ptr = torch.empty(max_hubs + 1, dtype=torch.int32, device=dev)
+    hub_dst = torch.empty(max_hubs, dtype=torch.int32, device=dev)
+    nh, nc = _lib.c_i64(0), _lib.c_i64(0)
+    if n > 0:
+        ws = _ws(lib.gfd_plan_workspace_size(n), dev)
+        _lib.call("gfd_plan_hubs", rowptr.data_ptr(), n, threshold, chunk, hub_rank.data_ptr(),
+                  hub_chunk.data_ptr(), hub_chunk_ptr.data_ptr(), hub_dst.data_ptr(), max_hubs,
+                  max_chunks, _lib.ct.byref(nh), _lib.ct.byref(nc), ws.data_ptr(), ws.numel(),
+                  _lib.stream_handle(dev))
+    return (hub_rank, hub_chunk[:4 * nc.value], hub_chunk_ptr[:nh.value + 1], hub_dst[:nh.value],
+            nh.value, nc.value)
+
+
+def hub_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = SRC_HUB_THRESHOLD,
+             chunk: int = SRC_HUB_CHUNK) -> Plan:
+    """A plan with only the hub split (the backward's source hubs over the CSC
+    ``colptr``)."""
+    hub_rank, hub_chunk, hub_chunk_ptr, hub_dst, nh, nc = _hubs(rowptr, num_messages, threshold,
+                                                                chunk)
+    return Plan(rowptr.numel() - 1, None, None, None, hub_rank, hub_chunk, hub_chunk_ptr, hub_dst,
+                nh, nc, None)
 
 
 @dataclass
@@ -133,6 +157,7 @@ class CSC:
     colptr: torch.Tensor
     dst: torch.Tensor
     eid: torch.Tensor
+    plan: Optional[Plan] = None   # source hubs (hub_plan over colptr)
 
 
 @dataclass
@@ -166,7 +191,7 @@ class CSRGraph:
             _lib.call("gfd_csc_from_csr", self.rowptr.data_ptr(), self.col.data_ptr(), M, N,
                       colptr.data_ptr(), dst.data_ptr(), eid.data_ptr(), ws.data_ptr(),
                       ws.numel(), _lib.stream_handle(self.device))
-            self._csc = CSC(colptr, dst, eid)
+            self._csc = CSC(colptr, dst, eid, hub_plan(colptr, M))
         return self._csc
 
     def shard(self, lo: int, hi: int) -> "CSRShard":

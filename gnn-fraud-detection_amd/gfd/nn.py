@@ -87,9 +87,6 @@ class GATConvFunction(torch.autograd.Function):
         slope, dp, seed, has_bias = ctx.meta
         dev = x.device
         g = grad_out.contiguous().to(torch.float32)
-        xin = x
-        if x.dtype != torch.float32:  # bf16 features: the backward reads fp32 rows
-            x = x.float()
         N, F = x.shape
         H, C = SUPPORTED_HEADS, weight.size(0) // SUPPORTED_HEADS
         csc = graph.csc()
@@ -99,17 +96,19 @@ class GATConvFunction(torch.autograd.Function):
         gad = torch.empty_like(att_dst)
         gb = torch.empty((C,), dtype=torch.float32, device=dev) if has_bias else None
         lib = _lib.load()
-        ws = _ws(lib.gfd_gat_bwd_workspace_size(N, graph.num_messages, F, H, C), dev)
+        plan, splan = graph.plan(), csc.plan
+        ws = _ws(lib.gfd_gat_bwd_workspace_size(N, graph.num_messages, F, H, C, plan.num_hubs,
+                                                plan.num_chunks, splan.num_chunks), dev)
         _lib.call("gfd_gat_bwd", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
-                  graph.rowptr.data_ptr(),
-                  graph.col.data_ptr(), csc.colptr.data_ptr(), csc.dst.data_ptr(),
-                  csc.eid.data_ptr(), graph.num_messages, weight.data_ptr(), att_src.data_ptr(),
+                  graph.rowptr.data_ptr(), graph.col.data_ptr(), plan.cstruct(),
+                  csc.colptr.data_ptr(), csc.dst.data_ptr(), csc.eid.data_ptr(), splan.cstruct(),
+                  graph.num_messages, weight.data_ptr(), att_src.data_ptr(),
                   att_dst.data_ptr(), H, C, slope, dp, seed & (2 ** 64 - 1), st.data_ptr(),
                   stats.data_ptr(), g.data_ptr(), _lib.ptr(gx), gw.data_ptr(), gas.data_ptr(),
                   gad.data_ptr(), _lib.ptr(gb), ws.data_ptr(), ws.numel(),
                   _lib.stream_handle(dev))
-        if gx is not None and xin.dtype != torch.float32:
-            gx = gx.to(xin.dtype)
+        if gx is not None and x.dtype != torch.float32:
+            gx = gx.to(x.dtype)
         return gx, gw, gas, gad, gb, None, None, None, None
 
 

@@ -238,19 +238,25 @@ gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t num_nodes, int in_fea
                        float* st, float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
- * GATConv backward (autograd of the PyG dataflow).
- * Given grad_out [N, C], the forward's st [N, 2H] and stats [N, 2H], writes
- * grad_x [N, F] (nullable), grad_weight [H*C, F], grad_att_src/grad_att_dst
- * [H*C], grad_bias [C] (nullable).  All outputs are overwritten (not
- * accumulated).  Needs the CSR and its CSC view.
+ * GATConv backward (autograd of the PyG dataflow at loss.backward(),
+ * train.py:142).  Given grad_out [N, C], the forward's
+ * st [N, 2H] and stats [N, 2H], writes grad_x [N, F] (nullable), grad_weight
+ * [H*C, F], grad_att_src/grad_att_dst [H*C], grad_bias [C] (nullable).  All
+ * outputs are overwritten (not accumulated); deterministic (no float atomics).
+ * Like the forward it gathers x rows, never the projected rows: the attention
+ * gradient is <W_h^T grad_out_i / H, x_j>.  ``plan`` is the forward's plan
+ * (tile order + destination hub chunks; NULL = identity order, no hubs);
+ * ``src_plan`` (nullable) is a gfd_plan_hubs split of the CSC ``colptr``
+ * (source hubs; only its hub fields are read).  x may be fp32 or bf16.
  * ------------------------------------------------------------------------- */
 size_t gfd_gat_bwd_workspace_size(int64_t num_nodes, int64_t num_messages, int in_features,
-                                  int heads, int channels);
+                                  int heads, int channels, int64_t num_hubs, int64_t num_chunks,
+                                  int64_t num_src_chunks);
 
 gfd_status gfd_gat_bwd(const void* x, int x_dtype, int64_t num_nodes, int in_features,
-                       int64_t x_stride,
-                       const int32_t* rowptr, const int32_t* col, const int32_t* colptr,
-                       const int32_t* csc_dst, const int32_t* csc_eid, int64_t num_messages,
+                       int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                       const gfd_plan* plan, const int32_t* colptr, const int32_t* csc_dst,
+                       const int32_t* csc_eid, const gfd_plan* src_plan, int64_t num_messages,
                        const float* weight, const float* att_src, const float* att_dst,
                        int heads, int channels, float negative_slope, float dropout_p,
                        uint64_t dropout_seed, const float* st, const float* stats,

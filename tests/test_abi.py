@@ -61,7 +61,7 @@ def test_workspace_queries(lib):
     big = lib.gfd_gat_fwd_workspace_size(1000, 1000, 166, 8, 64, 10, 100)
     assert big > small > 0
     assert lib.gfd_csr_workspace_size(10_000, 1000) >= 4 * 4 * 10_000
-    assert lib.gfd_gat_bwd_workspace_size(1000, 5000, 166, 8, 64) >= 2 * 1000 * 512 * 4
+    assert lib.gfd_gat_bwd_workspace_size(1000, 5000, 166, 8, 64, 0, 0, 0) >= 1000 * 528 * 4
 
 
 def test_argument_errors_without_launch(lib):
@@ -78,11 +78,16 @@ def test_argument_errors_without_launch(lib):
     args[11] = 8
     args[0], args[1] = ctypes.addressof(x), 7                # unknown x_dtype
     assert lib.gfd_gat_fwd(*args) == 1
-    # gfd_gat_bwd: bf16 features are not accepted by the backward (fp32 rows)
-    bargs = ([ctypes.addressof(x), 1, 1, 1, 1] + [None] * 5 + [1] + [None] * 3 +
+    # gfd_gat_bwd: 32 parameters; bf16 x accepted, an unknown dtype and null
+    # operands rejected before any launch
+    bargs = ([ctypes.addressof(x), 1, 1, 1, 1] + [None] * 7 + [1] + [None] * 3 +
              [8, 64, 0.2, 0.0, 0] + [None] * 8 + [None, 0, None])
-    assert len(bargs) == len(lib.gfd_gat_bwd.argtypes)
-    assert lib.gfd_gat_bwd(*bargs) == 5
+    assert len(bargs) == len(lib.gfd_gat_bwd.argtypes) == 32
+    assert lib.gfd_gat_bwd(*bargs) == 1
+    bargs[1] = 7
+    assert lib.gfd_gat_bwd(*bargs) == 1
+    bargs[1], bargs[16] = 0, 4
+    assert lib.gfd_gat_bwd(*bargs) == 5                      # heads != 8
 
 
 def test_missing_library_fails_loudly(tmp_path):

@@ -127,6 +127,46 @@ def test_backward_vs_oracle_elliptic_like():
     assert_close_scaled(b.grad, conv.bias.grad, what="grad_bias")
 
 
+def _grads(gnn, x, ei, conv, g):
+    xd = x.to(DEV).requires_grad_(True)
+    ps = [t.detach().to(DEV).requires_grad_(True)
+          for t in (conv.lin_src.weight, conv.att_src, conv.att_dst, conv.bias)]
+    (gnn.gat_conv(xd, ei.to(DEV), *ps) * g.to(DEV)).sum().backward()
+    return [xd.grad] + [p.grad for p in ps]
+
+
+def test_backward_is_deterministic():
+    """No float atomics: grad_W (split-K over 40k nodes), grad_att and
+    grad_bias (per-block partials) come out bit-identical run to run."""
+    gnn, _ = _gfd()
+    x, ei, conv = _random_case(40000, 300000, 166, seed=21)
+    g = torch.randn(40000, 64, generator=torch.Generator().manual_seed(5))
+    a = _grads(gnn, x, ei, conv, g)
+    b = _grads(gnn, x, ei, conv, g)
+    for name, u, v in zip(("x", "W", "att_src", "att_dst", "bias"), a, b):
+        assert torch.equal(u, v), f"grad_{name} differs between two identical backward calls"
+
+
+def test_backward_bf16_features():
+    """bf16 x goes straight into the backward (rows converted on load): the
+    gradients equal the fp32 oracle's on the bf16-rounded features."""
+    gnn, _ = _gfd()
+    x, ei, conv = _random_case(3000, 24000, 166, seed=22)
+    xb = x.to(torch.bfloat16)
+    g = torch.randn(3000, 64, generator=torch.Generator().manual_seed(6))
+    xr = xb.float().requires_grad_(True)
+    (conv(xr, ei) * g).sum().backward()
+    gx, gW, gas, gad, gb = _grads(gnn, xb, ei, conv, g)
+    assert gx.dtype == torch.bfloat16
+    assert_close_scaled(gW, conv.lin_src.weight.grad, what="grad_W (bf16 x)")
+    assert_close_scaled(gas, conv.att_src.grad, what="grad_att_src (bf16 x)")
+    assert_close_scaled(gad, conv.att_dst.grad, what="grad_att_dst (bf16 x)")
+    assert_close_scaled(gb, conv.bias.grad, what="grad_bias (bf16 x)")
+    # grad_x is returned in x's dtype: compare at bf16 resolution
+    assert torch.allclose(gx.float().cpu(), xr.grad.to(torch.bfloat16).float(),
+                          rtol=2 ** -7, atol=1e-3 * xr.grad.abs().max().item())
+
+
 @pytest.mark.parametrize("threshold,chunk", [(1, 1), (4, 3), (16, 16), (1 << 30, 128)])
 @pytest.mark.parametrize("classes", [False, True])
 def test_hub_split_equivalence(threshold, chunk, classes):
