@@ -126,6 +126,10 @@ class Layer:
         self.xmax = torch.zeros(1, dtype=torch.float32, device=dev)
         self.stream = _lib.stream_handle(dev)
         self.cplan = self.plan.cstruct()
+        # one shard = the whole graph: the lone destinations' outputs come out of
+        # the logits pass (gfd_gat_logits_lone) and the tile stage skips that class
+        self.fused = spec.dst_lo == 0 and spec.dst_hi == self.N and world == 1
+        self.stages = self.STAGES_FUSED if self.fused else self.STAGES
 
     def pack_and_logits(self):
         s, _lib, F = self.s, self._lib, self.s["F"]
@@ -133,7 +137,12 @@ class Layer:
                   s["a_d"].data_ptr(), F, H, C, self.packed.data_ptr(), self.stream)
         self.xmax.zero_()
         x, spec = s["x"], s["spec"]
-        if self.world == 1:
+        if self.fused:
+            _lib.call("gfd_gat_logits_lone", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
+                      self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
+                      s["bias"].data_ptr(), 0.2, self.st.data_ptr(), self.xmax.data_ptr(),
+                      self.out.data_ptr(), None, self.stream)
+        elif self.world == 1:
             _lib.call("gfd_gat_logits_ex", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
                       self.packed.data_ptr(), H, C, self.st.data_ptr(), self.xmax.data_ptr(),
                       self.stream)
@@ -159,10 +168,12 @@ class Layer:
 
     STAGES = (("pack+logits", None), ("hubs", STAGE_HUBS), ("general", STAGE_MID),
               ("light", STAGE_LIGHT), ("lone", STAGE_LONE))
+    STAGES_FUSED = (("pack+logits+lone", None), ("hubs", STAGE_HUBS), ("general", STAGE_MID),
+                    ("light", STAGE_LIGHT))
 
     def step(self, evs=None):
         # events record on torch's current stream == the stream every gfd launch uses
-        for k, (_, stg) in enumerate(self.STAGES):
+        for k, (_, stg) in enumerate(self.stages):
             if evs:
                 evs[k].record()
             if stg is None:
@@ -176,7 +187,7 @@ class Layer:
 def time_layer(layer, steps, warmup, world):
     for _ in range(warmup):
         layer.step()
-    nst = len(Layer.STAGES)
+    nst = len(layer.stages)
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst + 1)] for _ in range(steps)]
     torch.cuda.synchronize()
     if world > 1:
@@ -193,7 +204,7 @@ def time_layer(layer, steps, warmup, world):
     elapsed = time.perf_counter() - t0
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
     stage_ms = {name: med([e[k].elapsed_time(e[k + 1]) for e in events])
-                for k, (name, _) in enumerate(Layer.STAGES)}
+                for k, (name, _) in enumerate(layer.stages)}
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=layer.dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -216,18 +227,19 @@ def stage_bytes(s, plan, esz):
         hr = plan.hub_rank[:deg.numel()]
         hubs_mask = (hr[order] if order is not None else hr) >= 0
     t = 16
-    lb = (light_b + t - 1) // t * t
-    ob = (lone_b + t - 1) // t * t
+    lb = (light_b + t - 1) // t * t   # the general launch owns the rest of its last tile
     idx = torch.arange(sdeg.numel(), device=sdeg.device)
     gen = idx < lb
-    light = (idx >= lb) & (idx < ob)
-    lone = idx >= ob
+    light = (idx >= lb) & (idx < lone_b)
+    lone = idx >= lone_b
     row_b = F * esz + 4
     W_b = 4 * F * H * C
     hub_msgs = int(sdeg[hubs_mask].sum().item())
     out_b = 4 + 4 * C
     res = {
         "pack+logits": s["graph"].num_nodes * (F * esz + 64) + W_b,
+        "pack+logits+lone": s["graph"].num_nodes * (F * esz + 64 + 4) + W_b +
+                            int(lone.sum().item()) * out_b,
         "hubs": hub_msgs * row_b + plan.num_chunks * 4 * (16 + 8 * ((F + 7) // 8 * 8)),
         "general": int(sdeg[gen & ~hubs_mask].sum().item()) * row_b +
                    int(gen.sum().item()) * out_b + W_b,
@@ -330,7 +342,9 @@ def measure(args, dev, rank, world, config):
         kernels[name] = {"ms": ms, "algorithmic_bytes": sb[name], "gbps": gbps,
                          "frac": gbps / HBM_PEAK_GBPS}
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
-    kname = {"pack+logits": "k_logits_s (+ pack)", "hubs": "k_hub_partial + k_hub_fin",
+    kname = {"pack+logits": "k_logits_s (+ pack)",
+             "pack+logits+lone": "k_logits_lone (+ pack): logits + self-loop-only rows",
+             "hubs": "k_hub_partial + k_hub_fin",
              "general": "k_stream<general> (hub rows, 5+ messages)",
              "light": "k_stream<light> (2-4 messages)",
              "lone": "k_lone (self-loop-only rows)"}

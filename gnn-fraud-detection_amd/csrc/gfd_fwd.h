@@ -33,7 +33,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // Packed weights (gfd_gat_pack_weights).
 struct PackLayout {
   int F, Fp, Fu, KP, KS, KB;
-  size_t hdr_off, uv_off, whi_off, wlo_off, wsh_off, wsl_off, wbh_off, wbl_off, bytes;
+  size_t hdr_off, uv_off, whi_off, wlo_off, wsh_off, wsl_off, wbh_off, wbl_off, wph_off, wpl_off,
+      bytes;
 };
 
 inline PackLayout pack_layout(int F) {
@@ -56,6 +57,10 @@ inline PackLayout pack_layout(int F) {
   // head-mean matrix Wbar = mean_h W_h (k_lone): K position p = f, lo unscaled
   L.wbh_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 4 * 64, 256);
   L.wbl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 4 * 64, 256);
+  // the same matrix in the logits pass's lane order (k_logits_lone): in k-step t
+  // lane group g holds features 32 t + 4 g .. +3 and 32 t + 16 + 4 g .. +3
+  L.wph_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 4 * 64, 256);
+  L.wpl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 4 * 64, 256);
   L.bytes = o;
   return L;
 }
@@ -81,6 +86,18 @@ struct XBF16 {
 
 __device__ __forceinline__ float xcvt(float v) { return v; }
 __device__ __forceinline__ float xcvt(uint16_t v) { return __uint_as_float(uint32_t(v) << 16); }
+
+// Four consecutive features of one row as fp32 (16-B fp32 / 8-B bf16 load).
+template <typename XT>
+__device__ __forceinline__ f32x4 load4(const typename XT::T* p) {
+  if constexpr (XT::kBytes == 4) {
+    return *reinterpret_cast<const f32x4*>(p);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                 __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+  }
+}
 
 // x row j as a byte pointer: an unsigned 32 x 32 -> 64-bit product (two scalar
 // multiplies instead of a sign-extended 64-bit one); j >= 0 and the row pitch
@@ -389,6 +406,12 @@ gfd_status launch_lone(const AggArgs& a, const PackLayout& L, hipStream_t stream
 gfd_status launch_fused(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_logits(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
                          const float* uv, int Fu, float* st, float* xmax, hipStream_t stream);
+// logits fused with the lone destinations' outputs (gfd_logits.hip)
+bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx);
+gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
+                              const PackLayout& L, const char* packed, const int32_t* rowptr,
+                              const float* bias, float slope, float* st, float* xmax, float* out,
+                              float* stats, hipStream_t stream);
 
 inline int kf_for(int F) { return (F + 63) / 64; }
 

@@ -93,6 +93,16 @@ gfd_status tiles_impl(const AggArgs& a, const PackLayout& L, hipStream_t stream)
   return (lone && (cls & kLoneBit)) ? launch_lone(a, L, stream) : GFD_OK;
 }
 
+// The whole-graph forward may take the lone class out of the tile stage and
+// into the logits pass (k_logits_lone): exactly when the tile stage would run
+// the class-scheduled kernels with a lone class.
+bool lone_fusable(const AggArgs& a, const PackLayout& L) {
+  const gfd_plan& p = a.plan;
+  return kf_for(a.F) <= 3 && L.KB <= 6 && p.slot_desc && p.slot_cols && p.class_split &&
+         a.dp == 0.f && a.slope >= 0.f && a.slope <= 1.f && a.dst_offset == 0 &&
+         a.num_dst == a.N && logits_lone_supported(a.x, a.xdt, a.F, a.ldx);
+}
+
 gfd_status aggregate_impl(const AggArgs& a, hipStream_t stream) {
   const PackLayout L = pack_layout(a.F);
   if (a.stages & GFD_STAGE_HUBS) {
@@ -221,8 +231,17 @@ gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t N, int F, int64_t ldx
   s = gfd_gat_pack_weights(weight, att_src, att_dst, F, heads, channels, packed, stream_);
   if (s != GFD_OK) return s;
   if (hipMemsetAsync(xmax, 0, sizeof(float), stream) != hipSuccess) return GFD_ERR_HIP;
-  s = gfd_gat_logits_ex(x, x_dtype, N, F, ldx, packed, heads, channels, st, xmax, stream_);
-  if (s != GFD_OK) return s;
+  if (lone_fusable(a, L)) {
+    // the lone destinations' outputs come out of the logits pass; the tile
+    // stage runs the general and light classes only
+    s = launch_logits_lone(x, x_dtype, N, F, ldx, L, a.packed, rowptr, bias, slope, st, xmax,
+                           out, stats, stream);
+    if (s != GFD_OK) return s;
+    a.stages = GFD_STAGE_HUBS | GFD_STAGE_TILES_GENERAL | GFD_STAGE_TILES_LIGHT;
+  } else {
+    s = gfd_gat_logits_ex(x, x_dtype, N, F, ldx, packed, heads, channels, st, xmax, stream_);
+    if (s != GFD_OK) return s;
+  }
   return aggregate_impl(a, stream);
 }
 

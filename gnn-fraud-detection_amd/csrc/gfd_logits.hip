@@ -1,0 +1,231 @@
+// gfd_logits.hip -- the per-node attention logits pass of PyG GATConv.forward
+// (alpha_src / alpha_dst; /root/reference/src/models/gat.py:80, tgn.py:94)
+// fused with the outputs of the destinations whose only message is their own
+// self loop ("lone": a third of the C4 power-law graph's nodes).
+//
+// A lone destination's softmax has one term, alpha = 1 for every head, so
+// PyG's out_i = mean_h W_h x_i + bias = Wbar x_i + bias.  The logits pass
+// already streams every row of x through registers; computing Wbar x_i there
+// (K = F on f16 MFMA, 3-term hi/lo split of the power-of-two scaled row,
+// ~2^-21 relative) for the rows whose in-degree is 1 saves the lone kernel's
+// second read of those rows.
+//
+// k_logits_lone: 8-wave blocks, two per CU, grid-stride over 16-row tiles.
+//   * lane (r = l & 15, g = l >> 4) loads features 16 s + 4 g .. +3 of row r
+//     for every fp32 k-step s (16-B loads, all issued before the first MFMA);
+//   * st = x . [U | V] on v_mfma_f32_16x16x4_f32 (exact fp32 chains, the same
+//     arithmetic as k_logits_s) with the folded logit vectors in LDS;
+//   * if any row of the tile is lone: the row scaled by 2^e (max |x| ->
+//     [2^13, 2^14)), split into f16 hi / lo', and out = x . Wbar^T on
+//     v_mfma_f32_16x16x32_f16 -- f16 k-step t is exactly fp32 k-steps 2t and
+//     2t+1 of the lane, matched by the permuted Wbar fragments (k_pack_wbar_perm)
+//     that stay in LDS for the launch;
+//   * out rows (and, in training, the softmax stats: max = leaky(s_i + t_i),
+//     denominator 1) are written for lone rows only.
+#include "gfd_fwd.h"
+
+using namespace gfd;
+using namespace gfd::fwd;
+
+namespace {
+
+constexpr int kLLWaves = 8;  // 512-thread blocks, two per CU (LDS 60 KB each)
+constexpr int kLKS = 12;     // fp32 k-steps of 16 features (F <= 192)
+constexpr int kLKB = 6;      // f16 k-steps of 32 features
+
+// KS fp32 k-steps held per row (11: F <= 176, the f16 k-step 5 pairs step 10
+// with zeros; 12: F <= 192)
+template <typename XT, int KS>
+__global__ void __launch_bounds__(kLLWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_logits_lone(
+    const typename XT::T* __restrict__ x, int64_t rows, int F, int64_t ldx,
+    const float* __restrict__ uv, int Fu, const PackHeader* __restrict__ hdr,
+    const uint4* __restrict__ wph, const uint4* __restrict__ wpl,
+    const int32_t* __restrict__ rowptr, const float* __restrict__ bias, float slope,
+    float* __restrict__ st, float* __restrict__ xmax, float* __restrict__ out,
+    float* __restrict__ stats) {
+  __shared__ uint4 WB[2][kLKB][4][64];  // permuted Wbar hi / lo fragments, zero past KB
+  __shared__ f32x4 UV[kLKS][64];        // logit vectors in the B layout of each k-step
+  const int KB = (F + 31) / 32;
+  const int kst = (F + 15) / 16;  // fp32 k-steps incl. the ragged tail
+  const int ksf = F / 16;         // fp32 k-steps fully inside the row
+  for (int i = threadIdx.x; i < kLKB * 4 * 64; i += blockDim.x) {
+    const bool in = i < KB * 4 * 64;
+    WB[0][0][0][i] = in ? wph[i] : make_uint4(0, 0, 0, 0);
+    WB[1][0][0][i] = in ? wpl[i] : make_uint4(0, 0, 0, 0);
+  }
+  for (int i = threadIdx.x; i < kLKS * 64; i += blockDim.x) {
+    const int s = i >> 6, l = i & 63;
+    UV[s][l] = s < kst ? *reinterpret_cast<const f32x4*>(uv + (l & 15) * Fu + 16 * s + 4 * (l >> 4))
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int rl = lane & 15, g = lane >> 4;
+  const float wbu = hdr->wb_unscale;
+  float am = 0.f;  // max |x| over the values this lane loaded
+  const int64_t wave = int64_t(blockIdx.x) * kLLWaves + (threadIdx.x >> 6);
+  const int64_t nwave = int64_t(gridDim.x) * kLLWaves;
+  const int64_t tiles = (rows + 15) / 16;
+  for (int64_t t = wave; t < tiles; t += nwave) {
+    const int64_t row = t * 16 + rl;
+    const bool rin = row < rows;
+    const typename XT::T* xr = x + (rin ? row : rows - 1) * ldx + 4 * g;
+    f32x4 a[kLKS];
+#pragma unroll
+    for (int s = 0; s < kLKS; ++s) {
+      if (s >= KS) {
+        a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      if (s < ksf) {
+        a[s] = load4<XT>(xr + 16 * s);
+      } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[s][u] = 16 * s + 4 * g + u < F ? xcvt(xr[16 * s + u]) : 0.f;
+      } else {
+        a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    const bool lone = rin && rowptr[row + 1] - rowptr[row] == 1;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s < kst) {
+        const f32x4 b = UV[s][lane];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][u], b[u], acc, 0, 0, 0);
+      }
+    }
+    float rm = 0.f;  // max |x| of this lane's part of the row
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      rm = fmaxf(fmaxf(rm, fmaxf(fabsf(a[s].x), fabsf(a[s].y))), fmaxf(fabsf(a[s].z), fabsf(a[s].w)));
+    am = fmaxf(am, rm);  // clamped tail rows repeat row rows - 1: harmless for a max
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t orow = t * 16 + 4 * g + r;
+      if (orow < rows) st[orow * 16 + rl] = acc[r];
+    }
+    if (__ballot(lone) == 0) continue;  // wave-uniform: no lone row in this tile
+    const int er = scale_exp(max_xor16_32(rm));  // lanes r, r + 16, r + 32, r + 48
+    const float rs = ldexpf(1.0f, er);
+    f32x4 o[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tt = 0; tt < kLKB; ++tt) {
+      union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4& src = a[2 * tt + (i >> 1)];
+        const f32x2 v = f32x2{src[2 * (i & 1)], src[2 * (i & 1) + 1]} * f32x2{rs, rs};
+        hi.p[i] = __builtin_convertvector(v, f16x2);
+        lo.u[i] = split_lo(v, hi.u[i]);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
+        const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+        const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+        o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, o[ct], 0, 0, 0);
+        o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, o[ct], 0, 0, 0);
+        o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, o[ct], 0, 0, 0);
+      }
+    }
+    // o[ct] element q of lane l: row 4 g + q, column 16 ct + rl
+    const float uns = ldexpf(1.0f, -er) * wbu;
+    const int lone_i = lone ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int src = 4 * g + q;  // a lane holding row src's flag and scale
+      const int lq = __builtin_amdgcn_ds_bpermute(src << 2, lone_i);
+      const float uq = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(uns)));
+      // the row's t logits (columns 8..15) next to its s logits (0..7)
+      const float tq = dpp_mov<0x128>(acc[q]);  // row_ror:8 within the 16-lane row
+      if (lq) {
+        const int64_t orow = t * 16 + src;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+          out[orow * C + ct * 16 + rl] = o[ct][q] * uq + (bias ? bias[ct * 16 + rl] : 0.f);
+        if (__builtin_expect(stats != nullptr, 0) && rl < H) {  // training (no dropout) only
+          stats[orow * 16 + rl] = leaky(acc[q] + tq, slope);
+          stats[orow * 16 + H + rl] = 1.0f;
+        }
+      }
+    }
+  }
+  if (xmax) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+    if (lane == 0)  // non-negative floats order like their bit patterns
+      atomicMax(reinterpret_cast<unsigned int*>(xmax), __float_as_uint(am));
+  }
+}
+
+template <typename XT>
+gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackLayout& L,
+                    const char* packed, const int32_t* rowptr, const float* bias, float slope,
+                    float* st, float* xmax, float* out, float* stats, hipStream_t stream) {
+  const int64_t tiles = (rows + 15) / 16;
+  int64_t nb = (tiles + kLLWaves - 1) / kLLWaves;
+  const int64_t cap = int64_t(cu_count()) * 2;  // resident blocks; grid-stride beyond
+  if (nb > cap) nb = cap;
+  auto kern = F <= 176 ? &k_logits_lone<XT, 11> : &k_logits_lone<XT, 12>;
+  kern<<<int(nb), kLLWaves * 64, 0, stream>>>(
+      static_cast<const typename XT::T*>(x), rows, F, ldx,
+      reinterpret_cast<const float*>(packed + L.uv_off), L.Fu,
+      reinterpret_cast<const PackHeader*>(packed + L.hdr_off),
+      reinterpret_cast<const uint4*>(packed + L.wph_off),
+      reinterpret_cast<const uint4*>(packed + L.wpl_off), rowptr, bias, slope, st, xmax, out,
+      stats);
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
+
+}  // namespace
+
+namespace gfd {
+namespace fwd {
+
+bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx) {
+  const int eb = xdt == GFD_DTYPE_BF16 ? 2 : 4;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(x);
+  return F >= 1 && F <= 16 * kLKS && a % (4 * eb) == 0 && ldx % 4 == 0;
+}
+
+gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
+                              const PackLayout& L, const char* packed, const int32_t* rowptr,
+                              const float* bias, float slope, float* st, float* xmax, float* out,
+                              float* stats, hipStream_t stream) {
+  if (rows <= 0) return GFD_OK;
+  if (!logits_lone_supported(x, xdt, F, ldx)) return GFD_ERR_UNSUPPORTED;
+  return xdt == GFD_DTYPE_BF16
+             ? launch_t<XBF16>(x, rows, F, ldx, L, packed, rowptr, bias, slope, st, xmax, out,
+                               stats, stream)
+             : launch_t<XF32>(x, rows, F, ldx, L, packed, rowptr, bias, slope, st, xmax, out,
+                              stats, stream);
+}
+
+}  // namespace fwd
+}  // namespace gfd
+
+extern "C" {
+
+gfd_status gfd_gat_logits_lone(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                               int64_t x_stride, const void* packed, int heads, int channels,
+                               const int32_t* rowptr, const float* bias, float negative_slope,
+                               float* st, float* xmax, float* out, float* stats,
+                               gfd_stream_t stream_) {
+  if (heads != H || channels != C || in_features < 1 || in_features > 256)
+    return GFD_ERR_UNSUPPORTED;
+  if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
+  if (num_nodes < 0 || x_stride < in_features) return GFD_ERR_ARGUMENT;
+  if (num_nodes > 0 && (!x || !packed || !rowptr || !st || !out)) return GFD_ERR_ARGUMENT;
+  const PackLayout L = pack_layout(in_features);
+  return launch_logits_lone(x, x_dtype, num_nodes, in_features, x_stride, L,
+                            static_cast<const char*>(packed), rowptr, bias, negative_slope, st,
+                            xmax, out, stats, static_cast<hipStream_t>(stream_));
+}
+
+}  // extern "C"

@@ -65,15 +65,16 @@ __global__ void __launch_bounds__(kLWaves * 64) k_lone(
   float bc[4];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct) bc[ct] = bias ? bias[ct * 16 + r] : 0.f;
-  // lone slots: [16 * ceil(split[1] / 16), num_dst) (the light kernel owns the
-  // rest of its last tile)
-  const int64_t s0 = (split[1] + kTile - 1) / kTile * kTile;
+  // lone slots: [split[1], num_dst) in 16-slot groups from 16 * floor(split[1] /
+  // 16) (the light kernel stops at split[1] when this kernel runs)
+  const int64_t s1 = split[1];
+  const int64_t s0 = s1 / kTile * kTile;
   const int64_t groups = num_dst > s0 ? (num_dst - s0 + kTile - 1) / kTile : 0;
   const int64_t wid = (int64_t(blockIdx.x) * kLWaves) + (threadIdx.x >> 6);
   const int64_t nw = int64_t(gridDim.x) * kLWaves;
   for (int64_t gi = wid; gi < groups; gi += nw) {
     const int64_t slot = s0 + gi * kTile + r;
-    const int row = slot < num_dst ? desc[slot].x : -1;
+    const int row = (slot >= s1 && slot < num_dst) ? desc[slot].x : -1;
     float a[KB][8];
     // the self loop's source is the destination itself: its GLOBAL row of x
     const typename XT::T* xr = x + (dst_offset + (row < 0 ? 0 : row)) * ldx;

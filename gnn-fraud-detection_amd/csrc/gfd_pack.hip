@@ -138,19 +138,38 @@ __global__ void k_pack_wbar(const float* __restrict__ W, int F, int KB,
   wbl[idx] = lo.v;
 }
 
-// ---------------------------------------------------------------------------
-// Four consecutive features of one row as fp32 (16-B fp32 / 8-B bf16 load).
-template <typename XT>
-__device__ __forceinline__ f32x4 load4(const typename XT::T* p) {
-  if constexpr (XT::kBytes == 4) {
-    return *reinterpret_cast<const f32x4*>(p);
-  } else {
-    const uint2 u = *reinterpret_cast<const uint2*>(p);
-    return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                 __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+// Head-mean fragments in the logits pass's lane order (k_logits_lone): lane
+// group g of k-step t holds, at positions j = 0..7, feature 32 t + 4 g + j
+// (j < 4) or 32 t + 16 + 4 g + j - 4 (j >= 4) -- exactly the features that
+// lane group's fp32 logits loads of k-steps 2 t and 2 t + 1 hold.
+__global__ void k_pack_wbar_perm(const float* __restrict__ W, int F, int KB,
+                                 const PackHeader* __restrict__ hdr, uint4* __restrict__ wph,
+                                 uint4* __restrict__ wpl) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (t, ct, lane)
+  if (idx >= KB * 4 * 64) return;
+  int lane = idx & 63, ct = (idx >> 6) & 3, t = idx >> 8;
+  int n = ct * 16 + (lane & 15), g = lane >> 4;
+  const float sc = hdr->wb_scale;
+  union { uint4 v; _Float16 h[8]; } hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int f = 32 * t + 4 * g + j + (j >= 4 ? 12 : 0);
+    float v = 0.f;
+    if (f < F) {
+      float acc = 0.f;
+#pragma unroll
+      for (int h = 0; h < H; ++h) acc += W[size_t(h * C + n) * F + f];
+      v = acc * (1.0f / H) * sc;
+    }
+    _Float16 hv = (_Float16)v;
+    hi.h[j] = hv;
+    lo.h[j] = (_Float16)(v - (float)hv);
   }
+  wph[idx] = hi.v;
+  wpl[idx] = lo.v;
 }
 
+// ---------------------------------------------------------------------------
 // st[r][q] = sum_f x[r][f] * uv[q][f] (q < 2H) on v_mfma_f32_16x16x4_f32 with the
 // 2H logit vectors stationary in registers (KSM k-steps of 16 features) and
 // all KSM x loads of a 16-row tile issued before the first MFMA.  Lane group
@@ -335,6 +354,10 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   k_pack_wbar<<<(n_wb + 255) / 256, 256, 0, stream>>>(weight, F, L.KB, hdr,
                                                       reinterpret_cast<uint4*>(p + L.wbh_off),
                                                       reinterpret_cast<uint4*>(p + L.wbl_off));
+  GFD_LAUNCH_CHECK();
+  k_pack_wbar_perm<<<(n_wb + 255) / 256, 256, 0, stream>>>(
+      weight, F, L.KB, hdr, reinterpret_cast<uint4*>(p + L.wph_off),
+      reinterpret_cast<uint4*>(p + L.wpl_off));
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }

@@ -73,14 +73,16 @@ struct SlotRows {  // a slot's first (and, for light slots, only) batch in fligh
   float xv[4][KF];  // x rows of messages 0..3 (lane <-> feature)
 };
 
-__device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst,
+// live: slot < lim (<= num_dst): the light launch stops at the first lone slot
+// when the lone rows are written elsewhere (k_lone, k_logits_lone)
+__device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst, int64_t lim,
                                        const int4* __restrict__ desc,
                                        const int32_t* __restrict__ cols8, int lane) {
   const int64_t sl = slot < num_dst ? slot : num_dst - 1;
   const int32_t* a = reinterpret_cast<const int32_t*>(desc + sl) + (lane & 3);
   const int32_t* b = cols8 + sl * 8 + (lane & 7);
   p.v = *((lane & 56) == 8 ? b : a);  // one dword per lane, one VGPR per slot
-  p.live = slot < num_dst;
+  p.live = slot < lim;
 }
 
 // One piece of the issue of a slot: part 0 = logits (t_i, s_j), the source
@@ -349,6 +351,9 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   const int64_t te = LIGHT ? ((to_end ? num_dst : split[1]) + kTile - 1) / kTile
                            : (split ? (split[0] + kTile - 1) / kTile : all);
   const int64_t nv = t0 < te - tb ? (te - tb - 1 - t0) / G + 1 : 0;
+  // light, not to the end: the slots of the last tile past split[1] are lone
+  // rows another kernel writes -- taken as empty here
+  const int64_t lim = (LIGHT && !to_end) ? split[1] : num_dst;
   int lane = opaque(threadIdx.x & 63);
   auto slot = [&](int64_t v, int r) { return (tb + t0 + v * G) * kTile + r; };
 
@@ -376,8 +381,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   SlotRec n0, n1;
   SlotRows<KF> d0, d1;
   // prologue: tile 0 issued and aggregated; records of tile 1 loading
-  sl_rec(n0, slot(0, r0), num_dst, desc, cols8, lane);
-  sl_rec(n1, slot(0, r1), num_dst, desc, cols8, lane);
+  sl_rec(n0, slot(0, r0), num_dst, lim, desc, cols8, lane);
+  sl_rec(n1, slot(0, r1), num_dst, lim, desc, cols8, lane);
 #define GFD_ISSUE(P, n, d, ring) \
   sl_issue_part<P, XT, KF, LIGHT>(n, d, x, ldx, F, col, st, dst_offset, ring, lane)
   GFD_ISSUE(0, n0, d0, ring0 + r0); GFD_ISSUE(1, n0, d0, ring0 + r0);
@@ -386,8 +391,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   GFD_ISSUE(0, n1, d1, ring0 + r1); GFD_ISSUE(1, n1, d1, ring0 + r1);
   GFD_ISSUE(2, n1, d1, ring0 + r1); GFD_ISSUE(3, n1, d1, ring0 + r1);
   GFD_ISSUE(4, n1, d1, ring0 + r1);
-  sl_rec(n0, slot(1, r0), num_dst, desc, cols8, lane);
-  sl_rec(n1, slot(1, r1), num_dst, desc, cols8, lane);
+  sl_rec(n0, slot(1, r0), num_dst, lim, desc, cols8, lane);
+  sl_rec(n1, slot(1, r1), num_dst, lim, desc, cols8, lane);
   auto aggregate = [&](int tpar) {  // this wave's two slots of the tile in parity tpar
     SlotRing* rg = ring0 + tpar * kTile;
     float* rsc = rsc0 + tpar * kTile;
@@ -461,7 +466,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       if (GFD_PIECE(3)) GFD_ISSUE(3, n0, d0, rg + r0);
       if (GFD_PIECE(4)) {
         GFD_ISSUE(4, n0, d0, rg + r0);
-        sl_rec(n0, slot(v + 2, r0), num_dst, desc, cols8, lane);
+        sl_rec(n0, slot(v + 2, r0), num_dst, lim, desc, cols8, lane);
       }
       if (GFD_PIECE(5)) GFD_ISSUE(0, n1, d1, rg + r1);
       if (GFD_PIECE(6)) GFD_ISSUE(1, n1, d1, rg + r1);
@@ -469,7 +474,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       if (GFD_PIECE(8)) GFD_ISSUE(3, n1, d1, rg + r1);
       if (GFD_PIECE(9)) {
         GFD_ISSUE(4, n1, d1, rg + r1);
-        sl_rec(n1, slot(v + 2, r1), num_dst, desc, cols8, lane);
+        sl_rec(n1, slot(v + 2, r1), num_dst, lim, desc, cols8, lane);
       }
 #undef GFD_PIECE
       if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1

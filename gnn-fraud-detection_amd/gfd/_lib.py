@@ -64,6 +64,8 @@ SIGNATURES = {
     "gfd_gat_logits": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),
     "gfd_gat_logits_ex": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P,
                                   P, P]),
+    "gfd_gat_logits_lone": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int,
+                                    P, P, c_f32, P, P, P, P, P]),
     "gfd_gat_fwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int, c_i64,
                                           c_i64]),
     "gfd_gat_aggregate": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P, P,

@@ -210,6 +210,23 @@ gfd_status gfd_gat_logits_ex(const void* x, int x_dtype, int64_t rows, int in_fe
                              int64_t x_stride, const void* packed, int heads, int channels,
                              float* st, float* xmax, gfd_stream_t stream);
 
+/* gfd_gat_logits_ex over a whole graph (rows = destinations = num_nodes) fused
+ * with the outputs of the destinations whose only message is their self loop
+ * (rowptr[i+1] - rowptr[i] == 1): their softmax has one term, so PyG's
+ * out_i = mean_h W_h x_i + bias, written to out[i] (and, with stats, their
+ * softmax max leaky(s_i + t_i) and denominator 1).  Other rows of out are not
+ * touched; follow with gfd_gat_aggregate_ex(stages = HUBS | TILES_GENERAL |
+ * TILES_LIGHT), which then leaves the lone class alone.  No dropout (with
+ * dropout alpha is not 1).  GFD_ERR_UNSUPPORTED when x's base or pitch is not
+ * 4-element aligned or F > 192 (use gfd_gat_logits_ex and the LONE stage).
+ * Replaces the same PyG GATConv.forward steps as gfd_gat_logits, plus the
+ * propagate of the self-loop-only destinations. */
+gfd_status gfd_gat_logits_lone(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                               int64_t x_stride, const void* packed, int heads, int channels,
+                               const int32_t* rowptr, const float* bias, float negative_slope,
+                               float* st, float* xmax, float* out, float* stats,
+                               gfd_stream_t stream);
+
 /* gfd_gat_aggregate with xmax (nullable) = max |x| over ALL rows of x.  Every
  * aggregated row is a convex combination of x rows (dropout: times 1/(1-p)),
  * so the tile stage then uses one power-of-two scale for every Z row instead
