@@ -115,8 +115,11 @@ __device__ __forceinline__ const char* xrow(const void* x, int j, int64_t ldx) {
 // instruction here consumes them.
 template <typename XT, int KF>
 __device__ __forceinline__ void row_regs(const char* xr, int F, int lane, bool ok, float (&v)[KF]) {
+  // ok is wave-uniform at every call; readfirstlane keeps the descriptor
+  // scalar when the compiler cannot prove it (else: a waterfall loop per load)
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<char*>(xr), 0, ok ? F * XT::kBytes : 0, 0x00020000);
+      const_cast<char*>(xr), 0, __builtin_amdgcn_readfirstlane(ok ? F * XT::kBytes : 0),
+      0x00020000);
 #pragma unroll
   for (int q = 0; q < KF; ++q) {
     if constexpr (XT::kBytes == 4) {
@@ -302,6 +305,27 @@ __device__ __forceinline__ void fma_rows(f32x2 (&z)[4][KF], const float (&xr)[NR
         for (int qq = 0; qq < KF; ++qq)
           z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
     }
+  }
+}
+
+// z = sum over the first K rows of p_k x_k (no per-message branches: rows past
+// the slot's messages carry p = 0 on valid prefetched rows)
+template <int KF, int K>
+__device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[4][KF], float pv) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    f32x2 p2[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * k + 2 * g);
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq)
+        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
   }
 }
 

@@ -121,27 +121,6 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF>& q,
   }
 }
 
-// z = sum over the first K rows of p_k x_k (no per-message branches: rows past
-// the slot's messages carry p = 0 on valid prefetched rows)
-template <int KF, int K>
-__device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[4][KF], float pv) {
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    f32x2 p2[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * k + 2 * g);
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int qq = 0; qq < KF; ++qq)
-        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
-  }
-}
-
 // A slot with at most 4 messages (all rows prefetched), not a hub, no dropout:
 // straight-line code, the softmax sum and reciprocal independent of the FMA
 // block.  kmax: messages to run (wave-uniform, >= n).
