@@ -38,7 +38,8 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
     const float* __restrict__ st, const PackHeader* __restrict__ hdr,
     const uint4* __restrict__ whi, const uint4* __restrict__ wlo, const float* __restrict__ bias,
     float slope, float dp, uint64_t seed, const int32_t* __restrict__ hub_rank,
-    const float* __restrict__ zhub, float* __restrict__ out, float* __restrict__ stats) {
+    const float* __restrict__ zhub, float* __restrict__ out, float* __restrict__ stats,
+    Epi ep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int KH4 = 4 * Fp;                 // K of one head-half
   const int ZS = KH4 + 8;                 // padded row stride (fp16 elements, 16 B pad)
@@ -184,7 +185,7 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
     for (int q = 0; q < 4; ++q) {
       const int r = (lane >> 4) * 4 + q;
       const int ri = rowid[r];
-      if (ri >= 0) out[int64_t(ri) * C + n] = accv[q] * (rscale[r] * wu) + b;
+      if (ri >= 0) out[int64_t(ri) * C + n] = epi_store_value(accv[q] * (rscale[r] * wu), b, n, ri, ep);
     }
   }
 }
@@ -206,7 +207,7 @@ gfd_status launch_fused_t(const AggArgs& a, const PackLayout& L, hipStream_t str
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.whi_off),
       reinterpret_cast<const uint4*>(a.packed + L.wlo_off), a.bias, a.slope, a.dp, a.seed,
-      p.num_hubs > 0 ? p.hub_rank : nullptr, a.zhub, a.out, a.stats);
+      p.num_hubs > 0 ? p.hub_rank : nullptr, a.zhub, a.out, a.stats, a.ep);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }

@@ -408,6 +408,30 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
 
 // ---------------------------------------------------------------------------
 // Host side.
+// Output epilogue of the reference layer body (gat.py:82-91, eval mode), applied
+// where the GATConv output row is stored: y = conv + bias, then
+//   y = y * a[n] + b[n]  (BatchNorm1d with running stats folded to an affine)
+//   y = max(y, 0)        (relu)
+//   y += res[row, n]     (residual: the layer input, same rows as out)
+// ab == NULL: plain GATConv output.  ab = [a[0..63] | b[0..63]].
+struct Epi {
+  const float* ab;
+  int relu;
+  const float* res;
+  int64_t ldr;
+};
+
+__device__ __forceinline__ float epi_store_value(float v, float bias_n, int n, int64_t row,
+                                                 const Epi& e) {
+  float y = v + bias_n;
+  if (e.ab) {
+    y = fmaf(y, e.ab[n], e.ab[C + n]);
+    if (e.relu) y = fmaxf(y, 0.f);
+    if (e.res) y += e.res[row * e.ldr + n];
+  }
+  return y;
+}
+
 struct AggArgs {
   const void* x; int xdt; int F; int64_t ldx;
   int64_t N;
@@ -416,6 +440,7 @@ struct AggArgs {
   gfd_plan plan; int stages; float* out; float* stats;
   float* part; float* zhub;
   const float* xmax;  // max |x| over all rows of x (nullable): one scale for every Z row
+  Epi ep;             // output epilogue (ep.ab == NULL: none)
 };
 
 int cu_count();
@@ -435,7 +460,7 @@ bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx);
 gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
                               const PackLayout& L, const char* packed, const int32_t* rowptr,
                               const float* bias, float slope, float* st, float* xmax, float* out,
-                              float* stats, hipStream_t stream);
+                              float* stats, const Epi& ep, hipStream_t stream);
 
 inline int kf_for(int F) { return (F + 63) / 64; }
 

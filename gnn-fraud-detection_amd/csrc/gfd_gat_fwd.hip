@@ -201,24 +201,30 @@ gfd_status gfd_gat_aggregate(const void* x, int x_dtype, int64_t N, int F, int64
                               stages, out, stats, ws, ws_bytes, stream_);
 }
 
-gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
-                       const int32_t* rowptr, const int32_t* col, const float* weight,
-                       const float* att_src, const float* att_dst, const float* bias, int heads,
-                       int channels, float slope, float dp, uint64_t seed, const gfd_plan* plan,
-                       float* out, float* st, float* stats, void* ws, size_t ws_bytes,
-                       gfd_stream_t stream_) {
+gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+                          const int32_t* rowptr, const int32_t* col, const float* weight,
+                          const float* att_src, const float* att_dst, const float* bias,
+                          int heads, int channels, float slope, float dp, uint64_t seed,
+                          const gfd_plan* plan, const gfd_epilogue* ep, float* out, float* st,
+                          float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   const gfd_plan p = plan_or_empty(plan);
   gfd_status s = check_agg_args(x, x_dtype, N, F, ldx, rowptr, col, N, 0, dp, p, out);
   if (s != GFD_OK) return s;
   if (!weight || !att_src || !att_dst) return GFD_ERR_ARGUMENT;
+  Epi e{nullptr, 0, nullptr, 0};
+  if (ep) {  // inference epilogue: no training statistics, no dropout
+    if (!ep->scale_shift || stats || dp > 0.f) return GFD_ERR_ARGUMENT;
+    if (ep->residual && ep->residual_stride < channels) return GFD_ERR_ARGUMENT;
+    e = Epi{ep->scale_shift, ep->relu ? 1 : 0, ep->residual, ep->residual_stride};
+  }
   if (ws_bytes < gfd_gat_fwd_workspace_size(N, N, F, heads, channels, p.num_hubs, p.num_chunks))
     return GFD_ERR_WORKSPACE;
   const PackLayout L = pack_layout(F);
   Carve c(ws, ws_bytes);
   AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p,
-            GFD_STAGE_ALL, out, stats, nullptr, nullptr, nullptr};
+            GFD_STAGE_ALL, out, stats, nullptr, nullptr, nullptr, e};
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.zhub);
   void* packed = c.take<char>(L.bytes);
   float* st_ws = c.take<float>(size_t(N) * 16);
@@ -235,7 +241,7 @@ gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t N, int F, int64_t ldx
     // the lone destinations' outputs come out of the logits pass; the tile
     // stage runs the general and light classes only
     s = launch_logits_lone(x, x_dtype, N, F, ldx, L, a.packed, rowptr, bias, slope, st, xmax,
-                           out, stats, stream);
+                           out, stats, a.ep, stream);
     if (s != GFD_OK) return s;
     a.stages = GFD_STAGE_HUBS | GFD_STAGE_TILES_GENERAL | GFD_STAGE_TILES_LIGHT;
   } else {
@@ -243,6 +249,17 @@ gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t N, int F, int64_t ldx
     if (s != GFD_OK) return s;
   }
   return aggregate_impl(a, stream);
+}
+
+gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+                       const int32_t* rowptr, const int32_t* col, const float* weight,
+                       const float* att_src, const float* att_dst, const float* bias, int heads,
+                       int channels, float slope, float dp, uint64_t seed, const gfd_plan* plan,
+                       float* out, float* st, float* stats, void* ws, size_t ws_bytes,
+                       gfd_stream_t stream_) {
+  return gfd_gat_fwd_ep(x, x_dtype, N, F, ldx, rowptr, col, weight, att_src, att_dst, bias, heads,
+                        channels, slope, dp, seed, plan, nullptr, out, st, stats, ws, ws_bytes,
+                        stream_);
 }
 
 }  // extern "C"

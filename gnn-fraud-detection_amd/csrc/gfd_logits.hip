@@ -43,7 +43,7 @@ k_logits_lone(
     const uint4* __restrict__ wph, const uint4* __restrict__ wpl,
     const int32_t* __restrict__ rowptr, const float* __restrict__ bias, float slope,
     float* __restrict__ st, float* __restrict__ xmax, float* __restrict__ out,
-    float* __restrict__ stats) {
+    float* __restrict__ stats, Epi ep) {
   __shared__ uint4 WB[2][kLKB][4][64];  // permuted Wbar hi / lo fragments, zero past KB
   __shared__ f32x4 UV[kLKS][64];        // logit vectors in the B layout of each k-step
   const int KB = (F + 31) / 32;
@@ -147,7 +147,8 @@ k_logits_lone(
         const int64_t orow = t * 16 + src;
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
-          out[orow * C + ct * 16 + rl] = o[ct][q] * uq + (bias ? bias[ct * 16 + rl] : 0.f);
+          out[orow * C + ct * 16 + rl] =
+              epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl, orow, ep);
         if (__builtin_expect(stats != nullptr, 0) && rl < H) {  // training (no dropout) only
           stats[orow * 16 + rl] = leaky(acc[q] + tq, slope);
           stats[orow * 16 + H + rl] = 1.0f;
@@ -166,7 +167,8 @@ k_logits_lone(
 template <typename XT>
 gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackLayout& L,
                     const char* packed, const int32_t* rowptr, const float* bias, float slope,
-                    float* st, float* xmax, float* out, float* stats, hipStream_t stream) {
+                    float* st, float* xmax, float* out, float* stats, const Epi& ep,
+                    hipStream_t stream) {
   const int64_t tiles = (rows + 15) / 16;
   int64_t nb = (tiles + kLLWaves - 1) / kLLWaves;
   const int64_t cap = int64_t(cu_count()) * 2;  // resident blocks; grid-stride beyond
@@ -178,7 +180,7 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
       reinterpret_cast<const PackHeader*>(packed + L.hdr_off),
       reinterpret_cast<const uint4*>(packed + L.wph_off),
       reinterpret_cast<const uint4*>(packed + L.wpl_off), rowptr, bias, slope, st, xmax, out,
-      stats);
+      stats, ep);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
@@ -197,14 +199,14 @@ bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx) {
 gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
                               const PackLayout& L, const char* packed, const int32_t* rowptr,
                               const float* bias, float slope, float* st, float* xmax, float* out,
-                              float* stats, hipStream_t stream) {
+                              float* stats, const Epi& ep, hipStream_t stream) {
   if (rows <= 0) return GFD_OK;
   if (!logits_lone_supported(x, xdt, F, ldx)) return GFD_ERR_UNSUPPORTED;
   return xdt == GFD_DTYPE_BF16
              ? launch_t<XBF16>(x, rows, F, ldx, L, packed, rowptr, bias, slope, st, xmax, out,
-                               stats, stream)
+                               stats, ep, stream)
              : launch_t<XF32>(x, rows, F, ldx, L, packed, rowptr, bias, slope, st, xmax, out,
-                              stats, stream);
+                              stats, ep, stream);
 }
 
 }  // namespace fwd
@@ -225,7 +227,8 @@ gfd_status gfd_gat_logits_lone(const void* x, int x_dtype, int64_t num_nodes, in
   const PackLayout L = pack_layout(in_features);
   return launch_logits_lone(x, x_dtype, num_nodes, in_features, x_stride, L,
                             static_cast<const char*>(packed), rowptr, bias, negative_slope, st,
-                            xmax, out, stats, static_cast<hipStream_t>(stream_));
+                            xmax, out, stats, Epi{nullptr, 0, nullptr, 0},
+                            static_cast<hipStream_t>(stream_));
 }
 
 }  // extern "C"

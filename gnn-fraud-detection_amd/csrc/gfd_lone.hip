@@ -52,7 +52,8 @@ __global__ void __launch_bounds__(kLWaves * 64) k_lone(
     int64_t dst_offset, const int4* __restrict__ desc, const float* __restrict__ st,
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ wbh,
     const uint4* __restrict__ wbl, const float* __restrict__ bias, float slope,
-    float* __restrict__ out, float* __restrict__ stats, const int64_t* __restrict__ split) {
+    float* __restrict__ out, float* __restrict__ stats, const int64_t* __restrict__ split,
+    Epi ep) {
   __shared__ uint4 WB[2][KB][4][64];  // Wbar hi / lo fragments [k-step][col tile][lane]
   for (int i = threadIdx.x; i < KB * 4 * 64; i += kLWaves * 64) {
     WB[0][0][0][i] = wbh[i];
@@ -118,7 +119,9 @@ __global__ void __launch_bounds__(kLWaves * 64) k_lone(
       const float ou = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(uns)));
       if (orow >= 0) {
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) out[int64_t(orow) * C + ct * 16 + r] = acc[ct][q] * ou + bc[ct];
+        for (int ct = 0; ct < 4; ++ct)
+          out[int64_t(orow) * C + ct * 16 + r] =
+              epi_store_value(acc[ct][q] * ou, bc[ct], ct * 16 + r, orow, ep);
       }
     }
     if (__builtin_expect(stats != nullptr, 0) && row >= 0) {  // training (no dropout) only
@@ -148,7 +151,7 @@ gfd_status launch_lone_k(const AggArgs& a, const PackLayout& L, hipStream_t stre
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wbh_off),
       reinterpret_cast<const uint4*>(a.packed + L.wbl_off), a.bias, a.slope, a.out, a.stats,
-      p.class_split);
+      p.class_split, a.ep);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }

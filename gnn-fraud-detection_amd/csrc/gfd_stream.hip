@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
     uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
     float* __restrict__ stats, const float* __restrict__ xmax,
-    const int64_t* __restrict__ split, int to_end) {
+    const int64_t* __restrict__ split, int to_end, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) char ssm[];
   const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
   const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     for (int q = 0; q < 4; ++q) {
       const int r = (lane >> 4) * 4 + q;
       const int ri = rid[r];
-      if (ri >= 0) out[int64_t(ri) * C + n] = sum[q] * (rsc[r] * wu) + bcol;
+      if (ri >= 0) out[int64_t(ri) * C + n] = epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep);
     }
   };
   f32x4 acc_prev = {0.f, 0.f, 0.f, 0.f};  // kh = 0: tile v - 1, stored during MFMA(v)
@@ -514,7 +514,7 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
-      a.zhub, a.out, a.stats, a.xmax, split, to_end ? 1 : 0);
+      a.zhub, a.out, a.stats, a.xmax, split, to_end ? 1 : 0, a.ep);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }

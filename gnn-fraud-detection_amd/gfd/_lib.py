@@ -21,6 +21,12 @@ P = ct.c_void_p
 
 
 
+class GfdEpilogue(ct.Structure):
+    """``gfd_epilogue`` (include/gfd.h)."""
+    _fields_ = [("scale_shift", P), ("relu", ct.c_int), ("residual", P),
+                ("residual_stride", c_i64)]
+
+
 class GfdPlan(ct.Structure):
     """``gfd_plan`` (include/gfd.h)."""
     _fields_ = [("row_order", P), ("slot_desc", P), ("slot_cols", P), ("hub_rank", P),
@@ -76,6 +82,11 @@ SIGNATURES = {
                                      ct.c_int, P, P, P, c_sz, P]),
     "gfd_gat_fwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,
                             ct.c_int, c_f32, c_f32, c_u64, PLAN, P, P, P, P, c_sz, P]),
+    "gfd_gat_fwd_ep": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,
+                               ct.c_int, c_f32, c_f32, c_u64, PLAN, ct.POINTER(GfdEpilogue), P, P,
+                               P, P, c_sz, P]),
+    "gfd_gru_head": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, ct.c_int, P,
+                             P, P]),
     "gfd_gat_bwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int, c_i64,
                                           c_i64, c_i64]),
     "gfd_gat_bwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, PLAN, P, P, P, PLAN, c_i64,

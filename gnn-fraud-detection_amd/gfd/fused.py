@@ -1,0 +1,104 @@
+"""Fused inference paths of the reference model bodies.
+
+* ``gat_layer`` -- one layer of /root/reference/src/models/gat.py:79-91 (and
+  tgn.py:93-105) in eval mode: GATConv -> BatchNorm1d(running stats) -> ReLU
+  -> dropout (identity) -> residual, as ONE call of ``gfd_gat_fwd_ep``: the
+  BatchNorm folds into a per-channel affine applied where the tile kernels
+  store each output row, so the layer output is written once (the unfused
+  path writes the GATConv output, then BN, ReLU and the residual add each
+  read and write [N, 64] again).
+* ``gru_head`` -- the TemporalGNN head (tgn.py:108-111): GRUCell(h, h0) +
+  Linear in one kernel (``gfd_gru_head``).
+
+Inference only: the calls refuse tensors that require grad (training needs
+the raw GATConv output for BatchNorm's batch statistics and autograd through
+the epilogue; gfd.models takes the unfused path then).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from .graph import CSRGraph, _ws, get_graph
+from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS, _rows
+
+H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
+
+
+def bn_affine(bn: Optional[torch.nn.BatchNorm1d], device) -> torch.Tensor:
+    """[2C] (scale | shift) of an eval-mode BatchNorm1d: y = x * scale + shift
+    with scale = gamma / sqrt(running_var + eps), shift = beta - mean * scale
+    (identity when ``bn`` is None)."""
+    if bn is None:
+        return torch.cat([torch.ones(C, device=device), torch.zeros(C, device=device)])
+    if not bn.track_running_stats or bn.running_var is None:
+        raise NotImplementedError("fused BatchNorm needs running statistics (eval mode)")
+    scale = torch.rsqrt(bn.running_var.float() + bn.eps)
+    if bn.affine:
+        scale = scale * bn.weight.float()
+    shift = -bn.running_mean.float() * scale
+    if bn.affine:
+        shift = shift + bn.bias.float()
+    return torch.cat([scale, shift]).contiguous()
+
+
+def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
+              residual: bool = False) -> torch.Tensor:
+    """One eval-mode layer body: residual(h) + relu(bn(conv(h, edge_index)))."""
+    if torch.is_grad_enabled() and (h.requires_grad or conv.lin_src.weight.requires_grad):
+        raise RuntimeError("gfd.fused.gat_layer is inference-only (use torch.no_grad())")
+    dev = h.device
+    graph = edge_index if isinstance(edge_index, CSRGraph) else get_graph(edge_index, h.size(0))
+    x = _rows(h)
+    N, F = x.shape
+    W = conv.lin_src.weight.detach().contiguous()
+    a_s = conv.att_src.detach().reshape(-1).contiguous()
+    a_d = conv.att_dst.detach().reshape(-1).contiguous()
+    bias = conv.bias.detach() if conv.bias is not None else None
+    ab = bn_affine(bn, dev)
+    res = None
+    if residual:
+        if F != C:
+            raise ValueError("residual needs the layer input width to equal 64")
+        res = x
+    ep = _lib.GfdEpilogue(ab.data_ptr(), 1 if relu else 0, _lib.ptr(res),
+                          res.stride(0) if res is not None else 0)
+    plan = graph.plan()
+    lib = _lib.load()
+    out = torch.empty((N, C), dtype=torch.float32, device=dev)
+    ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, plan.num_hubs, plan.num_chunks), dev)
+    _lib.call("gfd_gat_fwd_ep", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+              graph.rowptr.data_ptr(), graph.col.data_ptr(), W.data_ptr(), a_s.data_ptr(),
+              a_d.data_ptr(), _lib.ptr(bias), H, C, float(conv.negative_slope), 0.0, 0,
+              plan.cstruct(), _lib.ct.byref(ep), out.data_ptr(), None, None, ws.data_ptr(),
+              ws.numel(), _lib.stream_handle(dev))
+    return out
+
+
+def gru_head(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,
+             h0: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(lin(GRUCell(h, h0)), GRUCell(h, h0)) in one kernel (h0 None = zeros)."""
+    if torch.is_grad_enabled() and (h.requires_grad or gru.weight_ih.requires_grad):
+        raise RuntimeError("gfd.fused.gru_head is inference-only (use torch.no_grad())")
+    if gru.hidden_size != C or gru.input_size != C:
+        raise NotImplementedError("gfd gru_head: GRUCell(64, 64)")
+    dev = h.device
+    x = h if h.stride(1) == 1 and h.stride(0) % 4 == 0 else h.contiguous()
+    if h0 is not None:
+        h0 = h0 if h0.stride(1) == 1 and h0.stride(0) % 4 == 0 else h0.contiguous()
+    N = x.size(0)
+    O = lin.out_features
+    h_new = torch.empty((N, C), dtype=torch.float32, device=dev)
+    out = torch.empty((N, O), dtype=torch.float32, device=dev)
+    w_ih, w_hh = gru.weight_ih.detach().contiguous(), gru.weight_hh.detach().contiguous()
+    b_ih = gru.bias_ih.detach() if gru.bias else None
+    b_hh = gru.bias_hh.detach() if gru.bias else None
+    w_o = lin.weight.detach().contiguous()
+    b_o = lin.bias.detach() if lin.bias is not None else None
+    _lib.call("gfd_gru_head", x.data_ptr(), N, C, x.stride(0), w_ih.data_ptr(), _lib.ptr(b_ih),
+              w_hh.data_ptr(), _lib.ptr(b_hh), _lib.ptr(h0), h0.stride(0) if h0 is not None else 0,
+              w_o.data_ptr(), _lib.ptr(b_o), O, h_new.data_ptr(), out.data_ptr(),
+              _lib.stream_handle(dev))
+    return out, h_new

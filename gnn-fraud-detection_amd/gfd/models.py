@@ -8,7 +8,10 @@ constructor arguments, same submodule names (so ``results/gat_model.pt`` and
 difference is the GATConv underneath: ``gfd.nn.GATConv`` (libgfd.so).
 
 The per-layer epilogue is the reference's: GATConv -> BatchNorm1d -> ReLU ->
-dropout -> residual when widths match (gat.py:79-91).
+dropout -> residual when widths match (gat.py:79-91).  In inference (eval mode
+under no_grad) each layer is one fused call (BN folded into the GATConv store
+epilogue, ``gfd.fused.gat_layer``) and the TemporalGNN head is one kernel
+(``gfd.fused.gru_head``); training runs the same ops unfused with autograd.
 
 ``forward_snapshots`` is config C3: the TGN forward over per-time-step
 snapshots (h0 = 0 per step, tgn.py:88-89).  Elliptic edges never cross time
@@ -44,8 +47,20 @@ class _GATStack(nn.Module):
         self.batch_norms = (nn.ModuleList(nn.BatchNorm1d(hidden_channels) for _ in widths)
                             if use_batch_norm else None)
 
+    def _fused(self) -> bool:
+        """Inference (eval mode, no autograd): each layer body runs as one
+        GATConv launch chain with BN/ReLU/residual in the store epilogue."""
+        return not self.training and not torch.is_grad_enabled()
+
     def encode(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         h = x
+        if self._fused():
+            from . import fused
+            for layer, conv in enumerate(self.gat_layers):
+                bn = self.batch_norms[layer] if self.batch_norms is not None else None
+                h = fused.gat_layer(conv, bn, h, edge_index, relu=True,
+                                    residual=self.residual and h.size(-1) == self.hidden_channels)
+            return h
         for layer, conv in enumerate(self.gat_layers):
             y = conv(h, edge_index)
             if self.batch_norms is not None:
@@ -86,9 +101,13 @@ class TemporalGNN(_GATStack):
 
     def forward(self, x, edge_index, batch: Optional[torch.Tensor] = None,
                 hidden_state: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        h = self.encode(x, edge_index)
+        if self._fused():
+            from . import fused
+            return fused.gru_head(self.gru, self.out, h, hidden_state)
         if hidden_state is None:
             hidden_state = x.new_zeros((x.size(0), self.hidden_channels))
-        new_hidden = self.gru(self.encode(x, edge_index), hidden_state)
+        new_hidden = self.gru(h, hidden_state)
         return self.out(new_hidden), new_hidden
 
     def predict(self, x, edge_index, batch=None, hidden_state=None,

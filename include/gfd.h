@@ -254,6 +254,46 @@ gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t num_nodes, int in_fea
                        float dropout_p, uint64_t dropout_seed, const gfd_plan* plan, float* out,
                        float* st, float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream);
 
+/* Inference epilogue of the reference layer body (gat.py:82-91 and tgn.py
+ * :96-105 in eval mode: GATConv -> BatchNorm1d(running stats) -> ReLU ->
+ * dropout(identity) -> residual), applied by the kernels that store each
+ * output row, so the layer output is written once:
+ *   y = (conv + bias) * scale_shift[n] + scale_shift[C + n]
+ *   y = max(y, 0)                           if relu
+ *   y += residual[i * residual_stride + n]  if residual (the layer input)
+ * BatchNorm1d folds to scale = gamma / sqrt(running_var + eps) and
+ * shift = beta - running_mean * scale. */
+typedef struct gfd_epilogue {
+  const float* scale_shift; /* device [2 * C] */
+  int relu;
+  const float* residual;    /* device [N, residual_stride] or NULL */
+  int64_t residual_stride;
+} gfd_epilogue;
+
+/* gfd_gat_fwd followed by the epilogue (ep may be NULL = gfd_gat_fwd).  With
+ * an epilogue, stats must be NULL and dropout_p 0 (inference only: training
+ * needs the raw GATConv output for the BatchNorm batch statistics). */
+gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                          int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                          const float* weight, const float* att_src, const float* att_dst,
+                          const float* bias, int heads, int channels, float negative_slope,
+                          float dropout_p, uint64_t dropout_seed, const gfd_plan* plan,
+                          const gfd_epilogue* ep, float* out, float* st, float* stats, void* ws,
+                          size_t ws_bytes, gfd_stream_t stream);
+
+/* TemporalGNN head (tgn.py:108-111): h_new = GRUCell(h, h0) with PyTorch's
+ * gate order (r, z, n) and out = h_new W_out^T + b_out, one kernel (gate
+ * pre-activations stay on chip; exact fp32 MFMA products).  h [rows, C] with
+ * row stride h_stride (multiple of 4, 16-B aligned), w_ih / w_hh [3C, C],
+ * b_ih / b_hh [3C] (nullable), h0 (nullable = zeros, the reference's call,
+ * tgn.py:88-89), w_out [out_channels, C], b_out [out_channels] (nullable);
+ * h_new [rows, C], out [rows, out_channels].  C = 64. */
+gfd_status gfd_gru_head(const float* h, int64_t rows, int channels, int64_t h_stride,
+                        const float* w_ih, const float* b_ih, const float* w_hh,
+                        const float* b_hh, const float* h0, int64_t h0_stride,
+                        const float* w_out, const float* b_out, int out_channels, float* h_new,
+                        float* out, gfd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * GATConv backward (autograd of the PyG dataflow at loss.backward(),
  * train.py:142).  Given grad_out [N, C], the forward's

@@ -25,14 +25,17 @@ def test_gat_checkpoint_eval_matches_reference(golden):
     x = torch.from_numpy(arr["x"]).to(DEV)
     ei = torch.from_numpy(arr["edge_index"]).to(DEV)
     outs = []
-    hooks = [c.register_forward_hook(lambda mod, i, o: outs.append(o)) for c in m.gat_layers]
-    with torch.no_grad():
-        logits = m(x, ei)
+    hooks = [c.register_forward_hook(lambda mod, i, o: outs.append(o.detach())) for c in m.gat_layers]
+    logits_unfused = m(x, ei).detach()     # grad enabled: GATConv -> ATen BN/ReLU/residual
     for h in hooks:
         h.remove()
+    assert len(outs) == 3
     for i, o in enumerate(outs):
         assert_close(o, arr[f"gat_layer{i}"], what=f"GATConv layer {i}")
-    assert_close(logits, arr["gat_logits"], what="GAT logits")
+    assert_close(logits_unfused, arr["gat_logits"], what="GAT logits (unfused)")
+    with torch.no_grad():                  # inference: fused layer epilogues
+        logits = m(x, ei)
+    assert_close(logits, arr["gat_logits"], what="GAT logits (fused epilogues)")
 
 
 def test_tgn_checkpoint_eval_matches_reference(golden):
@@ -40,12 +43,62 @@ def test_tgn_checkpoint_eval_matches_reference(golden):
     m = _model("tgn", arr, "tgn.").eval()
     x = torch.from_numpy(arr["x"]).to(DEV)
     ei = torch.from_numpy(arr["edge_index"]).to(DEV)
-    with torch.no_grad():
+    with torch.no_grad():                  # fused layer epilogues + fused GRU/Linear head
         out, hid = m(x, ei)
         snap, _ = m.forward_snapshots(x, ei, torch.from_numpy(arr["time_step"]).to(DEV))
     assert_close(out, arr["tgn_out"], what="TGN out")
     assert_close(hid, arr["tgn_hidden"], what="TGN hidden")
     assert_close(snap, arr["tgn_out_snapshots"], what="TGN 49-step snapshots")
+    out_u, hid_u = m(x, ei)                # grad enabled: unfused path
+    assert_close(out_u.detach(), arr["tgn_out"], what="TGN out (unfused)")
+    assert_close(hid_u.detach(), arr["tgn_hidden"], what="TGN hidden (unfused)")
+
+
+@pytest.mark.parametrize("residual,relu,dtype", [(True, True, torch.float32),
+                                                 (False, True, torch.float32),
+                                                 (True, False, torch.bfloat16)])
+def test_fused_layer_epilogue_matches_unfused(residual, relu, dtype):
+    """gfd.fused.gat_layer (BN / ReLU / residual applied in the GATConv store
+    epilogue) against the same GATConv followed by ATen ops, with non-trivial
+    BatchNorm running statistics, on a graph with hubs, light and lone rows."""
+    from gfd import fused, synth
+    from gfd.nn import GATConv
+    torch.manual_seed(5)
+    N = 20000
+    ei = torch.from_numpy(synth.power_law(N, 160000, seed=5)).to(DEV)
+    x = torch.randn(N, 64, device=DEV).to(dtype)
+    conv = GATConv(64, 64, heads=8, concat=False).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    bn = torch.nn.BatchNorm1d(64).to(DEV).eval()
+    with torch.no_grad():
+        bn.running_mean.normal_()
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.normal_()
+        bn.bias.normal_()
+        ref = bn(conv(x, ei))
+        if relu:
+            ref = torch.relu(ref)
+        if residual:
+            ref = ref + x.float()
+        got = fused.gat_layer(conv, bn, x, ei, relu=relu, residual=residual)
+    assert_close(got, ref, what=f"fused layer residual={residual} relu={relu} {dtype}")
+
+
+@pytest.mark.parametrize("with_h0", [False, True])
+def test_fused_gru_head_matches_torch(with_h0):
+    from gfd import fused
+    torch.manual_seed(6)
+    gru = torch.nn.GRUCell(64, 64).to(DEV)
+    lin = torch.nn.Linear(64, 3).to(DEV)
+    h = torch.randn(5003, 64, device=DEV)
+    h0 = torch.randn(5003, 64, device=DEV) if with_h0 else None
+    with torch.no_grad():
+        hr = gru(h, h0 if h0 is not None else torch.zeros_like(h))
+        outr = lin(hr)
+        out, hn = fused.gru_head(gru, lin, h, h0)
+    assert_close(hn, hr, what="GRUCell h'")
+    assert_close(out, outr, what="Linear head")
 
 
 def test_gat_train_step_grads_match_reference(golden):
