@@ -65,6 +65,9 @@ SIGNATURES = {
     "gfd_order_workspace_size": (c_sz, [c_i64, c_i32]),
     "gfd_plan_order": (c_i32, [P, c_i64, c_i32, P, P, c_sz, P]),
     "gfd_plan_desc": (c_i32, [P, P, c_i64, P, P, P, P, P, P]),
+    "gfd_temporal_workspace_size": (c_sz, [c_i64, c_i64, c_i32]),
+    "gfd_temporal_snapshots": (c_i32, [P, c_i64, P, c_i64, c_i64, c_i32, P, P, P, P, P, P, P, c_sz,
+                                       P]),
     "gfd_gat_packed_size": (c_sz, [ct.c_int, ct.c_int, ct.c_int]),
     "gfd_gat_pack_weights": (c_i32, [P, P, P, ct.c_int, ct.c_int, ct.c_int, P, P]),
     "gfd_gat_logits": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),

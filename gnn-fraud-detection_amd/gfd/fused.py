@@ -62,7 +62,8 @@ def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
     if residual:
         if F != C:
             raise ValueError("residual needs the layer input width to equal 64")
-        res = x
+        # the epilogue adds fp32 rows (gfd_epilogue.residual is float*)
+        res = x if x.dtype == torch.float32 else x.float()
     ep = _lib.GfdEpilogue(ab.data_ptr(), 1 if relu else 0, _lib.ptr(res),
                           res.stride(0) if res is not None else 0)
     plan = graph.plan()
@@ -85,8 +86,10 @@ def gru_head(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,
     if gru.hidden_size != C or gru.input_size != C:
         raise NotImplementedError("gfd gru_head: GRUCell(64, 64)")
     dev = h.device
-    x = h if h.stride(1) == 1 and h.stride(0) % 4 == 0 else h.contiguous()
+    x = h.float() if h.dtype != torch.float32 else h      # the kernel reads fp32 rows
+    x = x if x.stride(1) == 1 and x.stride(0) % 4 == 0 else x.contiguous()
     if h0 is not None:
+        h0 = h0.float() if h0.dtype != torch.float32 else h0
         h0 = h0 if h0.stride(1) == 1 and h0.stride(0) % 4 == 0 else h0.contiguous()
     N = x.size(0)
     O = lin.out_features

@@ -117,9 +117,13 @@ class TemporalGNN(_GATStack):
 
     def forward_snapshots(self, x: torch.Tensor, edge_index: torch.Tensor,
                           time_step: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Config C3: per-time-step snapshot forwards (h0 = 0 each step) in one
-        launch.  Requires every edge to join two nodes of the same step (true
-        for Elliptic); raises otherwise."""
-        if (time_step[edge_index[0]] != time_step[edge_index[1]]).any():
-            raise ValueError("forward_snapshots: an edge crosses time steps")
-        return self.forward(x, edge_index)
+        """Config C3: the forward of every time-step snapshot (the reference's
+        create_temporal_subgraph per step, dataset.py:198-240, h0 = 0 per step,
+        tgn.py:88-89) in one launch chain: the snapshots are extracted on the
+        device (gfd.temporal) and run side by side as one graph that keeps only
+        intra-step edges, so every destination sees exactly its own step.
+        Exact per-snapshot semantics in eval mode (train-mode BatchNorm would
+        take batch statistics over all steps instead of one)."""
+        from .temporal import cached_snapshots
+        snap = cached_snapshots(time_step, edge_index, x.size(0))
+        return self.forward(x, snap.edge_index_intra)

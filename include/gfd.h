@@ -125,6 +125,27 @@ gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t num_
                          const int32_t* order, const int32_t* hub_rank, int32_t* desc,
                          int32_t* slot_cols, int64_t* class_split, gfd_stream_t stream);
 
+/* Per-time-step snapshots of a temporal graph, every step in one pass (config
+ * C3; replaces the reference's create_temporal_subgraph, dataset.py:198-240,
+ * called per step by create_temporal_dataloaders, dataloader.py:99-135).
+ * Steps are t_first .. t_first + num_steps - 1 of time_step[N] (int64).
+ *   node_perm[N]   nodes of step 0 in ascending id, then step 1, ...; nodes
+ *                  outside the steps last; node_pos[N] its inverse;
+ *   step_ptr[S+1]  offsets of each step's nodes in node_perm;
+ *   sub_edge_index [2, E] (row stride E): the edges whose endpoints are both in
+ *                  one step, grouped by step, original order inside a step,
+ *                  global node ids; sub_edge_local (nullable) the same edges
+ *                  with step-local ids (position in the step's node list);
+ *   edge_ptr[S+1]  offsets of each step's edges (edge_ptr[S] = kept edges).
+ * Validates indices (GFD_ERR_INDEX) and synchronises the stream once. */
+size_t gfd_temporal_workspace_size(int64_t num_nodes, int64_t num_edges, int32_t num_steps);
+gfd_status gfd_temporal_snapshots(const int64_t* time_step, int64_t num_nodes,
+                                  const int64_t* edge_index, int64_t num_edges, int64_t t_first,
+                                  int32_t num_steps, int32_t* node_perm, int32_t* node_pos,
+                                  int64_t* step_ptr, int64_t* sub_edge_index,
+                                  int64_t* sub_edge_local, int64_t* edge_ptr, void* ws,
+                                  size_t ws_bytes, gfd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * GATConv forward (PyG GATConv.forward, concat=False, add_self_loops=True,
  * bias=True; gat.py:80 / tgn.py:94):
