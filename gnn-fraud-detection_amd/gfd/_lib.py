@@ -68,6 +68,10 @@ SIGNATURES = {
     "gfd_temporal_workspace_size": (c_sz, [c_i64, c_i64, c_i32]),
     "gfd_temporal_snapshots": (c_i32, [P, c_i64, P, c_i64, c_i64, c_i32, P, P, P, P, P, P, P, c_sz,
                                        P]),
+    "gfd_sample_bounds": (c_i32, [c_i64, c_i64, P, c_i32, ct.POINTER(c_i64), ct.POINTER(c_i64)]),
+    "gfd_sample_workspace_size": (c_sz, [c_i64, c_i64, P, c_i32]),
+    "gfd_sample_neighbors": (c_i32, [P, P, c_i64, P, c_i64, P, c_i32, c_u64, P, P, P, P, P, P, P,
+                                     P, c_sz, P]),
     "gfd_gat_packed_size": (c_sz, [ct.c_int, ct.c_int, ct.c_int]),
     "gfd_gat_pack_weights": (c_i32, [P, P, P, ct.c_int, ct.c_int, ct.c_int, P, P]),
     "gfd_gat_logits": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),

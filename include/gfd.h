@@ -146,6 +146,32 @@ gfd_status gfd_temporal_snapshots(const int64_t* time_step, int64_t num_nodes,
                                   int64_t* sub_edge_local, int64_t* edge_ptr, void* ws,
                                   size_t ws_bytes, gfd_stream_t stream);
 
+/* Neighbour sampling for mini-batch training (replaces PyG NeighborLoader,
+ * dataloader.py:42-66: num_neighbors = fanouts[0..hops), batch_size seeds,
+ * sampling without replacement).  Hop l draws, for every node of frontier l,
+ * min(fanouts[l], in-degree) distinct in-neighbours (sources of edges into
+ * it) uniformly (Floyd's algorithm, counter-based random numbers keyed by
+ * (seed, hop, node, draw): deterministic per seed); new sources are appended
+ * in order of first appearance and form frontier l + 1.  The graph is the
+ * gfd_csr_from_coo CSR (its appended self loops are not sampled).
+ *   host fanouts[hops] (each <= 64); seeds[num_seeds] distinct node ids;
+ *   local_of[N] int32 scratch that must be all -1 (left all -1 on return);
+ *   n_id[max_nodes] global ids of the subgraph's nodes (seeds first);
+ *   level_ptr[hops + 2] node offsets per hop (level 0 = the seeds);
+ *   edge_src / edge_dst / edge_id[max_edges]: sampled edges, local ids of the
+ *   source and destination, and the edge's CSR position; edge_ptr[hops + 1].
+ * max_nodes / max_edges from gfd_sample_bounds.  Synchronises once. */
+gfd_status gfd_sample_bounds(int64_t num_nodes, int64_t num_seeds, const int32_t* fanouts,
+                             int32_t num_hops, int64_t* max_nodes, int64_t* max_edges);
+size_t gfd_sample_workspace_size(int64_t num_nodes, int64_t num_seeds, const int32_t* fanouts,
+                                 int32_t num_hops);
+gfd_status gfd_sample_neighbors(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
+                                const int64_t* seeds, int64_t num_seeds, const int32_t* fanouts,
+                                int32_t num_hops, uint64_t seed, int32_t* local_of, int64_t* n_id,
+                                int64_t* level_ptr, int64_t* edge_src, int64_t* edge_dst,
+                                int64_t* edge_id, int64_t* edge_ptr, void* ws, size_t ws_bytes,
+                                gfd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * GATConv forward (PyG GATConv.forward, concat=False, add_self_loops=True,
  * bias=True; gat.py:80 / tgn.py:94):
