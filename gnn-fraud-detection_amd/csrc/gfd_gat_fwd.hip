@@ -165,13 +165,13 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int
   return s.off;
 }
 
-gfd_status gfd_gat_aggregate_ex(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
                                 const int32_t* rowptr, const int32_t* col, int64_t num_dst,
                                 int64_t dst_offset, const float* st, const float* xmax,
                                 const void* packed, const float* bias, int heads, int channels,
                                 float slope, float dp, uint64_t seed, const gfd_plan* plan,
-                                int stages, float* out, float* stats, void* ws, size_t ws_bytes,
-                                gfd_stream_t stream_) {
+                                int stages, const gfd_epilogue* ep, float* out, float* stats,
+                                void* ws, size_t ws_bytes, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   const gfd_plan p = plan_or_empty(plan);
@@ -179,15 +179,33 @@ gfd_status gfd_gat_aggregate_ex(const void* x, int x_dtype, int64_t N, int F, in
       check_agg_args(x, x_dtype, N, F, ldx, rowptr, col, num_dst, dst_offset, dp, p, out);
   if (s != GFD_OK) return s;
   if (!st || !packed || stages < 1 || stages > 31) return GFD_ERR_ARGUMENT;
+  Epi e{nullptr, 0, nullptr, 0};
+  if (ep) {  // inference epilogue (see gfd_gat_fwd_ep); residual rows indexed like out
+    if (!ep->scale_shift || stats || dp > 0.f) return GFD_ERR_ARGUMENT;
+    if (ep->residual && ep->residual_stride < channels) return GFD_ERR_ARGUMENT;
+    e = Epi{ep->scale_shift, ep->relu ? 1 : 0, ep->residual, ep->residual_stride};
+  }
   if (num_dst == 0) return GFD_OK;
   const PackLayout L = pack_layout(F);
   AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, num_dst, dst_offset, st,
             static_cast<const char*>(packed), bias, slope, dp, seed, p, stages, out, stats,
-            nullptr, nullptr, xmax};
+            nullptr, nullptr, xmax, e};
   Carve c(ws, ws_bytes);
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.zhub);
   if (!c.ok && p.num_hubs > 0) return GFD_ERR_WORKSPACE;
   return aggregate_impl(a, stream);
+}
+
+gfd_status gfd_gat_aggregate_ex(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+                                const int32_t* rowptr, const int32_t* col, int64_t num_dst,
+                                int64_t dst_offset, const float* st, const float* xmax,
+                                const void* packed, const float* bias, int heads, int channels,
+                                float slope, float dp, uint64_t seed, const gfd_plan* plan,
+                                int stages, float* out, float* stats, void* ws, size_t ws_bytes,
+                                gfd_stream_t stream_) {
+  return gfd_gat_aggregate_ep(x, x_dtype, N, F, ldx, rowptr, col, num_dst, dst_offset, st, xmax,
+                              packed, bias, heads, channels, slope, dp, seed, plan, stages,
+                              nullptr, out, stats, ws, ws_bytes, stream_);
 }
 
 gfd_status gfd_gat_aggregate(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,

@@ -72,6 +72,11 @@ SIGNATURES = {
     "gfd_sample_workspace_size": (c_sz, [c_i64, c_i64, P, c_i32]),
     "gfd_sample_neighbors": (c_i32, [P, P, c_i64, P, c_i64, P, c_i32, c_u64, P, P, P, P, P, P, P,
                                      P, c_sz, P]),
+    "gfd_id_map_workspace_size": (c_sz, [c_i64]),
+    "gfd_id_map_build": (c_i32, [P, c_i64, P, P, P, c_sz, P]),
+    "gfd_id_map_lookup": (c_i32, [P, P, c_i64, P, c_i64, P, P]),
+    "gfd_edges_from_ids_workspace_size": (c_sz, [c_i64]),
+    "gfd_edges_from_ids": (c_i32, [P, P, c_i64, P, P, c_i64, P, P, P, c_sz, P]),
     "gfd_gat_packed_size": (c_sz, [ct.c_int, ct.c_int, ct.c_int]),
     "gfd_gat_pack_weights": (c_i32, [P, P, P, ct.c_int, ct.c_int, ct.c_int, P, P]),
     "gfd_gat_logits": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int, ct.c_int, P, P]),
@@ -87,6 +92,9 @@ SIGNATURES = {
     "gfd_gat_aggregate_ex": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P,
                                      P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, PLAN,
                                      ct.c_int, P, P, P, c_sz, P]),
+    "gfd_gat_aggregate_ep": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64, P,
+                                     P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, PLAN,
+                                     ct.c_int, ct.POINTER(GfdEpilogue), P, P, P, c_sz, P]),
     "gfd_gat_fwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,
                             ct.c_int, c_f32, c_f32, c_u64, PLAN, P, P, P, P, c_sz, P]),
     "gfd_gat_fwd_ep": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,

@@ -189,3 +189,101 @@ def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torc
     if gather_output:
         return all_gather_v_rows(out, spec.dst_bounds, group=group)
     return out
+
+
+# ---------------------------------------------------------------------------
+# Model-level sharding: every layer of the reference stack (gat.py:79-94,
+# tgn.py:93-111) destination-sharded, eval mode.
+
+def shard_aggregate_ep(h: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tensor,
+                       bias: Optional[torch.Tensor], spec: ShardSpec, negative_slope: float,
+                       xmax: Optional[torch.Tensor], scale_shift: torch.Tensor, relu: bool,
+                       residual: Optional[torch.Tensor]) -> torch.Tensor:
+    """shard_aggregate with the layer body's inference epilogue fused into the
+    output store (gfd_gat_aggregate_ep): BN(eval) affine, ReLU, residual rows
+    (``residual`` = the layer input rows of this shard's destinations)."""
+    from . import _lib
+    from .graph import _ws
+    from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
+    lib = _lib.load()
+    H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
+    N, F = h.shape
+    n_dst = spec.dst_hi - spec.dst_lo
+    out = torch.empty((n_dst, C), dtype=torch.float32, device=h.device)
+    if n_dst == 0:
+        return out
+    shard = graph.shard(spec.dst_lo, spec.dst_hi)
+    plan = shard.plan
+    ws = _ws(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, plan.num_hubs, plan.num_chunks),
+             h.device)
+    ep = _lib.GfdEpilogue(scale_shift.data_ptr(), 1 if relu else 0, _lib.ptr(residual),
+                          residual.stride(0) if residual is not None else 0)
+    _lib.call("gfd_gat_aggregate_ep", h.data_ptr(), _lib.x_dtype_code(h), N, F, h.stride(0),
+              shard.rowptr.data_ptr(), graph.col.data_ptr(), n_dst, spec.dst_lo, st.data_ptr(),
+              _lib.ptr(xmax), packed.data_ptr(), _lib.ptr(bias), H, C, float(negative_slope), 0.0,
+              0, plan.cstruct(), 3, _lib.ct.byref(ep), out.data_ptr(), None, ws.data_ptr(),
+              ws.numel(), _lib.stream_handle(h.device))
+    return out
+
+
+def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, residual: bool,
+                          group=None) -> torch.Tensor:
+    """One layer body on this rank: logits of the rank's node block, RCCL
+    all-gather of the [N, 16] logits (and max|x|), the rank's destinations
+    aggregated with BN / ReLU / residual in the store.  ``h`` is the layer
+    input for ALL N nodes (layer 0: the halo-resident features)."""
+    import torch.distributed as dist
+    from .fused import bn_affine
+    packed = pack_weights(conv.lin_src.weight.detach(), conv.att_src.detach(),
+                          conv.att_dst.detach())
+    xmax = torch.zeros(1, dtype=torch.float32, device=h.device)
+    st_local = shard_logits(h, packed, spec, xmax)
+    if spec.world > 1:
+        st = all_gather_rows(st_local, h.size(0), spec.world, group=group)
+        dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
+    else:
+        st = st_local
+    res = None
+    if residual:
+        res = h[spec.dst_lo:spec.dst_hi]
+        res = res if res.dtype == torch.float32 else res.float()
+    bias = conv.bias.detach() if conv.bias is not None else None
+    return shard_aggregate_ep(h, graph, st, packed, bias, spec, conv.negative_slope, xmax,
+                              bn_affine(bn, h.device), True, res)
+
+
+def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=None,
+                          gather_output: bool = True):
+    """Destination-sharded eval forward of gfd.models.GAT / TemporalGNN (the
+    reference's 2-3 layer stacks, gat.py:60-96, tgn.py:67-113) on this rank.
+
+    Layer 0 reads the halo-resident features (all N rows on every rank; the
+    exchange is the [N, 16] logits all-gather).  Layers >= 1 need the previous
+    layer's output for every source: one all-gather-v of the [n_dst, 64]
+    shards (2.56 GB in total at C4, one RCCL collective over xGMI).  The heads
+    (Linear, GRUCell + Linear) are row-local.  Returns the outputs of the
+    rank's destinations, or of all N nodes (gather_output).  Inference only."""
+    if model.training or torch.is_grad_enabled():
+        raise RuntimeError("model_forward_sharded is inference-only: model.eval() and no_grad")
+    h = x
+    L = len(model.gat_layers)
+    for layer, conv in enumerate(model.gat_layers):
+        bn = model.batch_norms[layer] if model.batch_norms is not None else None
+        res = model.residual and h.size(-1) == model.hidden_channels
+        out_local = layer_forward_sharded(conv, bn, h, graph, spec, res, group)
+        if layer < L - 1:
+            h = (all_gather_v_rows(out_local, spec.dst_bounds, group=group)
+                 if spec.world > 1 else out_local)
+        else:
+            h = out_local
+    if hasattr(model, "gru"):
+        from .fused import gru_head
+        out, hid = gru_head(model.gru, model.out, h)
+        if gather_output and spec.world > 1:
+            return (all_gather_v_rows(out, spec.dst_bounds, group=group),
+                    all_gather_v_rows(hid, spec.dst_bounds, group=group))
+        return out, hid
+    out = model.out(h)
+    if gather_output and spec.world > 1:
+        return all_gather_v_rows(out, spec.dst_bounds, group=group)
+    return out

@@ -74,6 +74,26 @@ gfd_status gfd_csr_from_coo(const int64_t* edge_index, int64_t num_edges, int64_
                             int32_t* rowptr, int32_t* col, void* ws, size_t ws_bytes,
                             gfd_stream_t stream);
 
+/* Graph ingest (replaces the id -> index dict and the per-row loops of
+ * EllipticBitcoinDataset.process, dataset.py:75-129).  gfd_id_map_build sorts
+ * (id, position) pairs of the node id column (stable: a repeated id maps to
+ * its LAST position, like the reference's dict comprehension, :92);
+ * gfd_id_map_lookup maps query ids to positions (-1 when unknown);
+ * gfd_edges_from_ids keeps the edges whose two endpoint ids are known, in
+ * their original order (:95-101), as int64 COO edge_index [2, E] (row stride
+ * E; the first *num_kept columns are written; num_kept is a device int64). */
+size_t gfd_id_map_workspace_size(int64_t num_ids);
+gfd_status gfd_id_map_build(const int64_t* ids, int64_t num_ids, int64_t* sorted_ids,
+                            int32_t* sorted_idx, void* ws, size_t ws_bytes, gfd_stream_t stream);
+gfd_status gfd_id_map_lookup(const int64_t* sorted_ids, const int32_t* sorted_idx, int64_t num_ids,
+                             const int64_t* queries, int64_t num_queries, int32_t* out,
+                             gfd_stream_t stream);
+size_t gfd_edges_from_ids_workspace_size(int64_t num_edges);
+gfd_status gfd_edges_from_ids(const int64_t* sorted_ids, const int32_t* sorted_idx,
+                              int64_t num_ids, const int64_t* src_ids, const int64_t* dst_ids,
+                              int64_t num_edges, int64_t* edge_index, int64_t* num_kept, void* ws,
+                              size_t ws_bytes, gfd_stream_t stream);
+
 /* 128-bit fingerprint of a COO edge list (two independent position-sensitive
  * 64-bit hashes of every (position, src, dst), device out[2]; no sync).  The
  * graph cache keys on it so that a re-uploaded but equal edge_index (the
@@ -340,6 +360,19 @@ gfd_status gfd_gru_head(const float* h, int64_t rows, int channels, int64_t h_st
                         const float* b_hh, const float* h0, int64_t h0_stride,
                         const float* w_out, const float* b_out, int out_channels, float* h_new,
                         float* out, gfd_stream_t stream);
+
+/* gfd_gat_aggregate_ex followed by the inference epilogue (ep nullable); the
+ * residual rows are indexed like out (destination dst_offset + i at row i).
+ * The destination-sharded model forward (gfd.dist) runs every layer through
+ * it. */
+gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                                int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                                int64_t num_dst, int64_t dst_offset, const float* st,
+                                const float* xmax, const void* packed, const float* bias,
+                                int heads, int channels, float negative_slope, float dropout_p,
+                                uint64_t dropout_seed, const gfd_plan* plan, int stages,
+                                const gfd_epilogue* ep, float* out, float* stats, void* ws,
+                                size_t ws_bytes, gfd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * GATConv backward (autograd of the PyG dataflow at loss.backward(),

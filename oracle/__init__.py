@@ -7,5 +7,6 @@ from .gatconv_ref import (GATConvRef, gatconv_forward, gatconv_forward_chunked, 
                           gatconv_forward_at, gatconv_forward_sampled,
                           remove_then_add_self_loops, segment_softmax, glorot_)
 from .models_ref import GATRef, TemporalGNNRef  # noqa: F401
+from .ingest_ref import process_ref  # noqa: F401
 from .sample_ref import floyd, sample_ref  # noqa: F401
 from .temporal_ref import temporal_subgraph_loop, temporal_subgraph_ref  # noqa: F401

@@ -1,0 +1,175 @@
+"""Model-level destination sharding (gfd.dist.model_forward_sharded; SURVEY.md
+§8e: layer 0 exchanges the [N, 16] logits, layers >= 1 all-gather the previous
+layer's [N, 64] output; BN / ReLU / residual fused into each shard's store).
+
+CPU (gloo, world 2 and 3): the orchestration -- collectives, shard bounds, the
+per-layer exchange and the epilogue arguments -- with the HIP stage functions
+replaced by oracle arithmetic in every worker; must equal the single-process
+reference model (oracle GATRef) in eval mode.
+GPU: the HIP stages of 2 / 3 virtual ranks run one after the other with their
+pieces concatenated as the all-gathers would, against the single-GPU fused
+forward and the oracle; and a world-1 RCCL group end to end."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from _util import assert_close, csr_cpu
+
+N, E, F, H, C = 500, 3000, 19, 8, 64
+
+
+def _problem():
+    from oracle import GATRef
+    g = torch.Generator().manual_seed(8)
+    w = torch.arange(1, N + 1, dtype=torch.float64) ** -0.8
+    dst = torch.multinomial(w, E, replacement=True, generator=g)
+    src = torch.randint(0, N, (E,), generator=g)
+    ei = torch.stack([src, dst])
+    x = torch.randn(N, F, generator=g)
+    torch.manual_seed(3)
+    m = GATRef(F, C, 1, num_layers=3).eval()
+    with torch.no_grad():
+        for bn in m.batch_norms:
+            bn.running_mean.normal_()
+            bn.running_var.uniform_(0.5, 2.0)
+        for conv in m.gat_layers:
+            conv.bias.normal_()
+    return ei, x, m
+
+
+def _patch_oracle_stages(gdist, ei):
+    """Replace the HIP stage functions by oracle arithmetic (CPU workers)."""
+    from oracle import gatconv_ref as ref
+
+    def pack_weights(W, a_s, a_d):
+        return {"W": W, "a_s": a_s, "a_d": a_d}
+
+    def shard_logits(h, packed, spec, xmax=None):
+        hh = (h[spec.node_lo:spec.node_hi] @ packed["W"].t()).view(-1, H, C)
+        a_s, a_d = packed["a_s"].view(1, H, C), packed["a_d"].view(1, H, C)
+        if xmax is not None and spec.node_hi > spec.node_lo:
+            xmax.copy_(torch.maximum(xmax, h[spec.node_lo:spec.node_hi].abs().max().view(1)))
+        return torch.cat([(hh * a_s).sum(-1), (hh * a_d).sum(-1)], 1)
+
+    def shard_aggregate_ep(h, graph, st, packed, bias, spec, slope, xmax, scale_shift, relu,
+                           residual):
+        rowptr, col = graph
+        y = ref.gatconv_forward_at(h, rowptr, col, torch.arange(spec.dst_lo, spec.dst_hi),
+                                   packed["W"], packed["a_s"].view(1, H, C),
+                                   packed["a_d"].view(1, H, C), bias)
+        y = y * scale_shift[:C] + scale_shift[C:]
+        if relu:
+            y = torch.relu(y)
+        return y + residual if residual is not None else y
+
+    gdist.pack_weights = pack_weights
+    gdist.shard_logits = shard_logits
+    gdist.shard_aggregate_ep = shard_aggregate_ep
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "gnn-fraud-detection_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from gfd import dist as gdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ei, x, m = _problem()
+        _patch_oracle_stages(gdist, ei)
+        rowptr, col = csr_cpu(ei, N)
+        spec = gdist.ShardSpec(rowptr, rank, world)
+        with torch.no_grad():
+            out = gdist.model_forward_sharded(m, x, (rowptr, col), spec)
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_model_sharded_orchestration_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ei, x, m = _problem()
+    with torch.no_grad():
+        want = m(x, ei)
+    assert_close(out, want, what=f"model sharded over {world} gloo ranks")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_model_virtual_ranks_match_single_gpu(world):
+    from gfd import dist as gdist, graph as ggraph
+    from gfd.fused import bn_affine
+    from gfd.models import GAT
+    dev = torch.device("cuda", 0)
+    ei, x, mref = _problem()
+    m = GAT(F, C, 1, num_layers=3).to(dev).eval()
+    m.load_state_dict(mref.state_dict(), strict=True)
+    g = ggraph.csr_from_coo(ei.to(dev), N)
+    specs = [gdist.ShardSpec(g.rowptr, r, world) for r in range(world)]
+    with torch.no_grad():
+        h = x.to(dev)
+        for layer, conv in enumerate(m.gat_layers):
+            packed = gdist.pack_weights(conv.lin_src.weight, conv.att_src, conv.att_dst)
+            xmax = torch.zeros(1, device=dev)
+            st = torch.cat([gdist.shard_logits(h, packed, s, xmax) for s in specs])
+            res = h.size(1) == C
+            h = torch.cat([gdist.shard_aggregate_ep(h, g, st, packed, conv.bias, s, 0.2, xmax,
+                                                    bn_affine(m.batch_norms[layer], dev), True,
+                                                    h[s.dst_lo:s.dst_hi] if res else None)
+                           for s in specs])
+        out = m.out(h)
+        single = m(x.to(dev), ei.to(dev))
+        want = mref(x, ei)
+    assert_close(out, single, what=f"{world} virtual ranks vs single GPU")
+    assert_close(out, want, what=f"{world} virtual ranks vs oracle")
+
+
+@pytest.mark.gpu
+def test_model_sharded_rccl_world1():
+    from gfd import dist as gdist, graph as ggraph
+    from gfd.models import GAT, TemporalGNN
+    dev = torch.device("cuda", 0)
+    ei, x, mref = _problem()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        g = ggraph.csr_from_coo(ei.to(dev), N)
+        spec = gdist.ShardSpec(g.rowptr, 0, 1)
+        m = GAT(F, C, 1, num_layers=3).to(dev).eval()
+        m.load_state_dict(mref.state_dict(), strict=True)
+        t = TemporalGNN(F, C, 1, num_layers=3).to(dev).eval()
+        with torch.no_grad():
+            out = gdist.model_forward_sharded(m, x.to(dev), g, spec)
+            tout, thid = gdist.model_forward_sharded(t, x.to(dev), g, spec)
+            tref, thref = t(x.to(dev), ei.to(dev))
+    finally:
+        dist.destroy_process_group()
+    with torch.no_grad():
+        want = mref(x, ei)
+    assert_close(out, want, what="GAT sharded world 1")
+    assert_close(tout, tref, what="TGN sharded world 1")
+    assert_close(thid, thref, what="TGN hidden sharded world 1")
