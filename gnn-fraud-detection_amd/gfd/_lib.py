@@ -102,6 +102,11 @@ SIGNATURES = {
                                P, P, c_sz, P]),
     "gfd_gru_head": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, ct.c_int, P,
                              P, P]),
+    "gfd_bn_workspace_size": (c_sz, []),
+    "gfd_bn_relu_fwd": (c_i32, [P, P, c_i64, ct.c_int, P, P, c_f32, c_f32, P, P, ct.c_int, c_f32,
+                                c_u64, P, P, P, P, c_sz, P]),
+    "gfd_bn_relu_bwd": (c_i32, [P, P, c_i64, ct.c_int, P, P, P, P, ct.c_int, c_f32, c_u64, P, P, P,
+                                P, c_sz, P]),
     "gfd_gat_bwd_workspace_size": (c_sz, [c_i64, c_i64, ct.c_int, ct.c_int, ct.c_int, c_i64,
                                           c_i64, c_i64]),
     "gfd_gat_bwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, PLAN, P, P, P, PLAN, c_i64,

@@ -10,9 +10,14 @@
 * ``gru_head`` -- the TemporalGNN head (tgn.py:108-111): GRUCell(h, h0) +
   Linear in one kernel (``gfd_gru_head``).
 
-Inference only: the calls refuse tensors that require grad (training needs
-the raw GATConv output for BatchNorm's batch statistics and autograd through
-the epilogue; gfd.models takes the unfused path then).
+* ``train_body`` -- the same layer body in training mode after the GATConv:
+  residual + dropout(relu(BatchNorm1d(y))) with batch statistics, as one
+  autograd Function over ``gfd_bn_relu_fwd`` / ``gfd_bn_relu_bwd`` (two
+  passes over y each way instead of ATen's BN / relu / dropout / add chain
+  and its saved intermediates; only y and two [64] vectors are kept).
+
+``gat_layer`` and ``gru_head`` are inference-only: they refuse tensors that
+require grad (gfd.models takes ``GATConv`` + ``train_body`` then).
 """
 from __future__ import annotations
 
@@ -105,3 +110,69 @@ def gru_head(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,
               w_o.data_ptr(), _lib.ptr(b_o), O, h_new.data_ptr(), out.data_ptr(),
               _lib.stream_handle(dev))
     return out, h_new
+
+
+class _BNReluDropout(torch.autograd.Function):
+    """out = res + dropout(relu(bn_train(y))); see include/gfd.h gfd_bn_relu_fwd."""
+
+    @staticmethod
+    def forward(ctx, y, res, gamma, beta, bn, relu, p, seed):
+        dev = y.device
+        N = y.size(0)
+        lib = _lib.load()
+        ws = _ws(lib.gfd_bn_workspace_size(), dev)
+        out = torch.empty_like(y)
+        mean = torch.empty(C, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        momentum = bn.momentum
+        if bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+            if momentum is None:  # cumulative moving average (torch BatchNorm semantics)
+                momentum = 1.0 / float(bn.num_batches_tracked.item())
+        rm = bn.running_mean if bn.track_running_stats else None
+        rv = bn.running_var if bn.track_running_stats else None
+        _lib.call("gfd_bn_relu_fwd", y.data_ptr(), _lib.ptr(res), N, C, _lib.ptr(gamma),
+                  _lib.ptr(beta), float(bn.eps), float(momentum or 0.0), _lib.ptr(rm),
+                  _lib.ptr(rv), 1 if relu else 0, float(p), seed, out.data_ptr(),
+                  mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), ws.numel(),
+                  _lib.stream_handle(dev))
+        ctx.save_for_backward(y, gamma, beta, mean, invstd)
+        ctx.relu, ctx.p, ctx.seed, ctx.has_res = relu, p, seed, res is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        y, gamma, beta, mean, invstd = ctx.saved_tensors
+        gout = gout.contiguous()
+        dev = y.device
+        lib = _lib.load()
+        ws = _ws(lib.gfd_bn_workspace_size(), dev)
+        gy = torch.empty_like(y)
+        gg = torch.empty(C, dtype=torch.float32, device=dev)
+        gb = torch.empty_like(gg)
+        _lib.call("gfd_bn_relu_bwd", y.data_ptr(), gout.data_ptr(), y.size(0), C,
+                  gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                  1 if ctx.relu else 0, float(ctx.p), ctx.seed, gy.data_ptr(), gg.data_ptr(),
+                  gb.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+        return (gy, gout if ctx.has_res else None, gg, gb, None, None, None, None)
+
+
+def train_supported(bn, y: torch.Tensor) -> bool:
+    """Whether ``train_body`` takes this layer: an affine training-mode
+    BatchNorm1d(64) over fp32 [N, 64] rows on the GPU."""
+    return (bn is not None and bn.training and bn.affine and y.is_cuda
+            and y.dtype == torch.float32 and y.dim() == 2 and y.size(1) == C and y.size(0) > 1
+            and bn.weight.dtype == torch.float32)
+
+
+def train_body(y: torch.Tensor, bn: torch.nn.BatchNorm1d, h: Optional[torch.Tensor],
+               relu: bool = True, p: float = 0.0) -> torch.Tensor:
+    """(h +) dropout(relu(bn(y)), p) in training mode (gat.py:82-91).  The
+    dropout mask is drawn from a seed taken from torch's CPU generator, so
+    ``torch.manual_seed`` makes it reproducible (it is not torch's own mask)."""
+    y = y.contiguous()
+    res = None
+    if h is not None:
+        res = h if (h.dtype == torch.float32 and h.is_contiguous()) else h.float().contiguous()
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+    return _BNReluDropout.apply(y, res, bn.weight, bn.bias, bn, relu, p, seed)

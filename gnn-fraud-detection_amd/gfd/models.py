@@ -11,7 +11,9 @@ The per-layer epilogue is the reference's: GATConv -> BatchNorm1d -> ReLU ->
 dropout -> residual when widths match (gat.py:79-91).  In inference (eval mode
 under no_grad) each layer is one fused call (BN folded into the GATConv store
 epilogue, ``gfd.fused.gat_layer``) and the TemporalGNN head is one kernel
-(``gfd.fused.gru_head``); training runs the same ops unfused with autograd.
+(``gfd.fused.gru_head``); in training the body after each GATConv (batch-
+statistics BN, ReLU, dropout, residual) is one autograd Function over two
+kernels each way (``gfd.fused.train_body``).
 
 ``forward_snapshots`` is config C3: the TGN forward over per-time-step
 snapshots (h0 = 0 per step, tgn.py:88-89).  Elliptic edges never cross time
@@ -63,6 +65,13 @@ class _GATStack(nn.Module):
             return h
         for layer, conv in enumerate(self.gat_layers):
             y = conv(h, edge_index)
+            bn = self.batch_norms[layer] if self.batch_norms is not None else None
+            if self.training and bn is not None:
+                from . import fused
+                if fused.train_supported(bn, y):
+                    res = h if (self.residual and h.size(-1) == y.size(-1)) else None
+                    h = fused.train_body(y, bn, res, relu=True, p=self.dropout)
+                    continue
             if self.batch_norms is not None:
                 y = self.batch_norms[layer](y)
             y = F.dropout(F.relu(y), p=self.dropout, training=self.training)

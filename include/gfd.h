@@ -401,6 +401,33 @@ gfd_status gfd_gat_bwd(const void* x, int x_dtype, int64_t num_nodes, int in_fea
                        float* grad_att_src, float* grad_att_dst, float* grad_bias, void* ws,
                        size_t ws_bytes, gfd_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Training-mode layer body (gat.py:82-91, tgn.py:96-105):
+ *   out = residual + dropout(relu(BatchNorm1d_train(y)))
+ * y [N, 64] fp32 (the GATConv output), residual nullable (fp32 rows [N, 64]).
+ * Batch statistics are reduced deterministically (two-level, fp64 partials);
+ * mean / invstd [64] are written for the backward; running_mean / running_var
+ * (nullable) are updated as torch.nn.BatchNorm1d does (unbiased variance,
+ * ``momentum`` weight on the batch value).  gamma / beta nullable = identity
+ * (the backward needs them).  Dropout is a counter-based mask of
+ * (seed, row * 64 + channel), regenerated by the backward; keep = 1/(1-p).
+ * gfd_bn_relu_bwd writes grad_y [N, 64] (the residual's gradient is grad_out
+ * itself) and grad_gamma / grad_beta [64] (nullable).
+ * ------------------------------------------------------------------------- */
+size_t gfd_bn_workspace_size(void);
+
+gfd_status gfd_bn_relu_fwd(const float* y, const float* residual, int64_t N, int channels,
+                           const float* gamma, const float* beta, float eps, float momentum,
+                           float* running_mean, float* running_var, int relu, float dropout_p,
+                           uint64_t seed, float* out, float* mean, float* invstd, void* ws,
+                           size_t ws_bytes, gfd_stream_t stream);
+
+gfd_status gfd_bn_relu_bwd(const float* y, const float* grad_out, int64_t N, int channels,
+                           const float* gamma, const float* beta, const float* mean,
+                           const float* invstd, int relu, float dropout_p, uint64_t seed,
+                           float* grad_y, float* grad_gamma, float* grad_beta, void* ws,
+                           size_t ws_bytes, gfd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

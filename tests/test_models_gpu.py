@@ -101,6 +101,71 @@ def test_fused_gru_head_matches_torch(with_h0):
     assert_close(out, outr, what="Linear head")
 
 
+@pytest.mark.parametrize("residual,relu", [(True, True), (False, True), (True, False)])
+def test_train_body_matches_torch(residual, relu):
+    """gfd.fused.train_body (batch-statistics BN -> ReLU -> residual, dropout 0)
+    against torch.nn.BatchNorm1d(train) + ATen: output, running statistics,
+    and the gradients of y, the residual input, gamma and beta."""
+    from gfd import fused
+    torch.manual_seed(8)
+    N = 30011
+    y0 = (torch.randn(N, 64, device=DEV) * 3 + 1).requires_grad_(True)
+    h0 = torch.randn(N, 64, device=DEV).requires_grad_(True)
+    bn_r = torch.nn.BatchNorm1d(64).to(DEV).train()
+    with torch.no_grad():
+        bn_r.weight.normal_()
+        bn_r.bias.normal_()
+    bn_g = torch.nn.BatchNorm1d(64).to(DEV).train()
+    bn_g.load_state_dict(bn_r.state_dict())
+    ref = bn_r(y0)
+    ref = torch.relu(ref) if relu else ref
+    ref = ref + h0 if residual else ref
+    g = torch.randn_like(ref)
+    gr = torch.autograd.grad(ref, [y0, h0, bn_r.weight, bn_r.bias], g, allow_unused=True)
+    y1 = y0.detach().clone().requires_grad_(True)
+    h1 = h0.detach().clone().requires_grad_(True)
+    got = fused.train_body(y1, bn_g, h1 if residual else None, relu=relu, p=0.0)
+    gg = torch.autograd.grad(got, [y1, h1, bn_g.weight, bn_g.bias], g, allow_unused=True)
+    assert_close(got, ref, what="train body out")
+    assert_close(bn_g.running_mean, bn_r.running_mean, what="running_mean")
+    assert_close(bn_g.running_var, bn_r.running_var, what="running_var")
+    assert int(bn_g.num_batches_tracked) == int(bn_r.num_batches_tracked) == 1
+    names = ["grad y", "grad residual", "grad gamma", "grad beta"]
+    for a, b, nm in zip(gg, gr, names):
+        if b is None:
+            assert a is None, nm
+        else:
+            assert_close_scaled(a, b, rtol=1e-4, what=nm)
+
+
+def test_train_body_dropout_mask():
+    """p > 0: the kept fraction is 1 - p, kept entries are scaled by 1/(1-p),
+    the same seed gives the same mask, and the backward uses that mask."""
+    from gfd import fused
+    torch.manual_seed(9)
+    N, p = 40000, 0.2
+    y = torch.randn(N, 64, device=DEV).requires_grad_(True)
+    bn = torch.nn.BatchNorm1d(64).to(DEV).train()
+    torch.manual_seed(10)
+    out = fused.train_body(y, bn, None, relu=False, p=p)
+    torch.manual_seed(10)
+    out2 = fused.train_body(y, torch.nn.BatchNorm1d(64).to(DEV).train(), None, relu=False, p=p)
+    assert torch.equal(out, out2)
+    with torch.no_grad():
+        z = torch.nn.functional.batch_norm(y, None, None, bn.weight, bn.bias, True, 0.0, bn.eps)
+    keep = out != 0
+    frac = keep.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.005, frac
+    assert_close(out[keep], (z / (1 - p))[keep], what="kept entries")
+    g = torch.randn_like(out)
+    (gy,) = torch.autograd.grad(out, [y], g)
+    yr = y.detach().clone().requires_grad_(True)
+    zr = torch.nn.functional.batch_norm(yr, None, None, bn.weight.detach(), bn.bias.detach(),
+                                        True, 0.0, bn.eps)
+    (gr,) = torch.autograd.grad(zr * keep.float() / (1 - p), [yr], g)
+    assert_close_scaled(gy, gr, rtol=1e-4, what="dropout backward")
+
+
 def test_gat_train_step_grads_match_reference(golden):
     """Config C2: fwd + BCE(pos_weight=50) + backward, dropout 0, train-mode BN."""
     arr = golden("gat3_train_grads.npz")
