@@ -66,17 +66,22 @@ __global__ void __launch_bounds__(kEB) k_col_stats(
   }
 }
 
-// one block: fixed-order sum of the partials -> out[0..127] (double)
-__global__ void __launch_bounds__(kC) k_col_final(const double* __restrict__ part, int parts,
-                                                  double* __restrict__ out) {
-  const int c = threadIdx.x;
-  double a = 0.0, b = 0.0;
-  for (int k = 0; k < parts; ++k) {
-    a += part[k * 2 * kC + c];
-    b += part[k * 2 * kC + kC + c];
+// one block of 1024 threads: thread (g, c) sums partials g, g + 8, ... of
+// column c (0..127: the a and b sums), then the 8 groups in order -- a fixed
+// order whatever the partial count
+__global__ void __launch_bounds__(1024) k_col_final(const double* __restrict__ part, int parts,
+                                                    double* __restrict__ out) {
+  __shared__ double red[8][2 * kC];
+  const int c = threadIdx.x & (2 * kC - 1), g = threadIdx.x >> 7;
+  double a = 0.0;
+  for (int k = g; k < parts; k += 8) a += part[k * 2 * kC + c];
+  red[g][c] = a;
+  __syncthreads();
+  if (threadIdx.x < 2 * kC) {
+    double t = 0.0;
+    for (int k = 0; k < 8; ++k) t += red[k][c];
+    out[c] = t;
   }
-  out[c] = a;
-  out[kC + c] = b;
 }
 
 // batch mean / biased var -> mean, invstd; running stats (unbiased var) update
@@ -177,7 +182,7 @@ gfd_status gfd_bn_relu_fwd(const float* y, const float* residual, int64_t N, int
   k_col_stats<<<g, kEB, 0, stream>>>(y, nullptr, nullptr, nullptr, nullptr, nullptr, N, 0, 0.f,
                                       0, part);
   GFD_LAUNCH_CHECK();
-  k_col_final<<<1, kC, 0, stream>>>(part, g, sums);
+  k_col_final<<<1, 1024, 0, stream>>>(part, g, sums);
   GFD_LAUNCH_CHECK();
   k_bn_moments<<<1, kC, 0, stream>>>(sums, N, eps, momentum, mean, invstd, running_mean,
                                      running_var);
@@ -205,7 +210,7 @@ gfd_status gfd_bn_relu_bwd(const float* y, const float* grad_out, int64_t N, int
   k_col_stats<<<g, kEB, 0, stream>>>(y, grad_out, mean, invstd, gamma, beta, N, relu ? 1 : 2,
                                       dropout_p, seed, part);
   GFD_LAUNCH_CHECK();
-  k_col_final<<<1, kC, 0, stream>>>(part, g, sums);
+  k_col_final<<<1, 1024, 0, stream>>>(part, g, sums);
   GFD_LAUNCH_CHECK();
   k_bn_bwd<<<egrid(N) * 4, kEB, 0, stream>>>(y, grad_out, N, mean, invstd, gamma, beta, sums,
                                               relu, dropout_p, seed, grad_y);

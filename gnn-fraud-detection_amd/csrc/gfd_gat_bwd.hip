@@ -23,7 +23,8 @@
 //                 in a fixed order by k_sum8
 //   k_bwd_src     one wave per source (CSC), chunks for source hubs: writes
 //                 dh' = [dh (512) | ds (8) | dt (8)] per node
-//   k_gemm_tn     grad_W' = dh'^T x (528 x F), split-K slabs + ordered reduce
+//   k_gw          grad_W' = dh'^T x (528 x F) on f16 MFMA (3-term split), split-K
+//                 slabs + ordered reduce
 //   k_att_grad    grad_att from the S / T rows of grad_W'
 //   k_gemm        grad_x = dh W (only when requested)
 // Deterministic: no float atomics anywhere; every sum has a fixed order.
@@ -437,45 +438,80 @@ __device__ __forceinline__ void src_segment(const int32_t* __restrict__ csc_dst,
   }
 }
 
-// dh' row j from y (lane = channel), ds (head lane & 7, complete) and dt_j
-__device__ __forceinline__ void write_dh(int64_t j, const float (&y)[H], float ds,
-                                         const float* __restrict__ dt,
-                                         const float* __restrict__ att_src,
-                                         const float* __restrict__ att_dst,
-                                         float* __restrict__ dh) {
+// dh' row j from y (lane = channel), ds (head lane & 7, complete) and dt_j;
+// returns the largest |value| the lane wrote (the grad_W' GEMM's scale)
+__device__ __forceinline__ float write_dh(int64_t j, const float (&y)[H], float ds,
+                                          const float* __restrict__ dt,
+                                          const float* __restrict__ att_src,
+                                          const float* __restrict__ att_dst,
+                                          float* __restrict__ dh) {
   const int lane = threadIdx.x & 63;
   float* r = dh + j * kDH;
   const float dtl = dt[j * 8 + (lane & 7)];
+  float mx = 0.f;
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     const float dsh = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ds), hh));
     const float dth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dtl), hh));
-    r[hh * C + lane] = fmaf(dth, att_dst[hh * C + lane],
-                            fmaf(dsh, att_src[hh * C + lane], y[hh] * (1.0f / H)));
+    const float v = fmaf(dth, att_dst[hh * C + lane],
+                         fmaf(dsh, att_src[hh * C + lane], y[hh] * (1.0f / H)));
+    r[hh * C + lane] = v;
+    mx = fmaxf(mx, fabsf(v));
   }
   if (lane < 8) {
     r[HC + lane] = ds;
     r[HC + H + lane] = dtl;
+    mx = fmaxf(mx, fmaxf(fabsf(ds), fabsf(dtl)));
+  }
+  return mx;
+}
+
+// amax[0] = max |dh'|, amax[1] = max |x| as float bits (non-negative floats
+// order like their bits; an integer max is exact and order-independent).
+// Block maximum first, and an atomic only when it beats the value already
+// there (thousands of same-address atomics otherwise serialise in L2).
+__device__ __forceinline__ void amax_commit(float dm, float xm, uint32_t* __restrict__ amax) {
+  __shared__ float red[2][16];
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  dm = max_wave(dm);
+  xm = max_wave(xm);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = dm;
+    red[1][w] = xm;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float m = 0.f;
+    for (int k = 0; k < nw; ++k) m = fmaxf(m, red[threadIdx.x][k]);
+    const uint32_t bits = __float_as_uint(m);
+    if (bits > __atomic_load_n(amax + threadIdx.x, __ATOMIC_RELAXED))
+      atomicMax(amax + threadIdx.x, bits);
   }
 }
 
+template <typename XT>
 __global__ void __launch_bounds__(256) k_bwd_src(
     const int32_t* __restrict__ colptr, const int32_t* __restrict__ csc_dst,
     const int32_t* __restrict__ csc_eid, int64_t N, const int32_t* __restrict__ src_hub_rank,
     const float* __restrict__ alpha_d, const float* __restrict__ dpre,
     const float* __restrict__ dt, const float* __restrict__ g, const float* __restrict__ att_src,
-    const float* __restrict__ att_dst, float* __restrict__ dh) {
+    const float* __restrict__ att_dst, const typename XT::T* __restrict__ x, int F, int64_t ldx,
+    float* __restrict__ dh, uint32_t* __restrict__ amax) {
+  const int lane = threadIdx.x & 63;
   const int64_t w0 = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  float dm = 0.f, xm = 0.f;
   for (int64_t j = w0; j < N; j += nw) {
+    for (int f = lane; f < F; f += 64) xm = fmaxf(xm, fabsf(ldx1(x + j * ldx + f)));
     if (src_hub_rank && src_hub_rank[j] >= 0) continue;  // k_bwd_src_hub
     float y[H];
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) y[hh] = 0.f;
     float ds = 0.f;
     src_segment(csc_dst, csc_eid, colptr[j], colptr[j + 1], alpha_d, dpre, g, y, ds);
-    write_dh(j, y, sum_xor8_16_32(ds), dt, att_src, att_dst, dh);
+    dm = fmaxf(dm, write_dh(j, y, sum_xor8_16_32(ds), dt, att_src, att_dst, dh));
   }
+  amax_commit(dm, xm, amax);
 }
 
 // source hub chunks {hub, p0, p1, src}: partial y (512) | ds (8) per chunk
@@ -505,7 +541,7 @@ __global__ void __launch_bounds__(512) k_bwd_src_hub2(
     const float* __restrict__ spart, const int32_t* __restrict__ chunk_ptr,
     const int32_t* __restrict__ hub_src, const float* __restrict__ dt,
     const float* __restrict__ att_src, const float* __restrict__ att_dst,
-    float* __restrict__ dh) {
+    float* __restrict__ dh, uint32_t* __restrict__ amax) {
   const int lane = threadIdx.x & 63, hh = threadIdx.x >> 6;
   const int64_t hb = blockIdx.x;
   const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
@@ -521,64 +557,204 @@ __global__ void __launch_bounds__(512) k_bwd_src_hub2(
   if (hh == 0 && lane < 8) sds[lane] = ds;
   __syncthreads();
   const float dth = dt[j * 8 + hh];
-  r[hh * C + lane] = fmaf(dth, att_dst[hh * C + lane],
-                          fmaf(sds[hh], att_src[hh * C + lane], y * (1.0f / H)));
+  const float v = fmaf(dth, att_dst[hh * C + lane],
+                       fmaf(sds[hh], att_src[hh * C + lane], y * (1.0f / H)));
+  r[hh * C + lane] = v;
+  float mx = fabsf(v);
   if (hh == 0 && lane < 8) {
+    const float dtl = dt[j * 8 + lane];
     r[HC + lane] = sds[lane];
-    r[HC + H + lane] = dt[j * 8 + lane];
+    r[HC + H + lane] = dtl;
+    mx = fmaxf(mx, fmaxf(fabsf(sds[lane]), fabsf(dtl)));
   }
+  amax_commit(mx, 0.f, amax);
 }
 
 // ---------------------------------------------------------------------------
-// grad_W' slabs: C_z[m][n] = sum_{k in split z} A[k][m] B[k][n] (both operands
-// k-major: A = dh' rows, B = x rows), fp32 MFMA 16x16x4.  Block tile 176 x 176
-// (11 waves, one 16-row strip each), BK = 16; m, n padded with zeros.
-constexpr int TT = 176, TK = 16, TW = 11;
+// grad_W' = dh'^T x  ([528, F], a sum over all N nodes) on f16 MFMA
+// 16x16x32 with the forward's 3-term split: both operands scaled by one power
+// of two each (max |dh'| and max |x| -> [2^13, 2^14), collected by k_bwd_src),
+// v = hi + lo in f16, acc += hi.hi + hi.lo + lo.hi (~2^-21 relative per
+// product; an fp32 MFMA 16x16x4 does 1/16 of the work per cycle).
+//  * block (8 waves) = one 176-row m-block of dh' x all Fu <= 256 feature
+//    columns over one K slab of nodes; partial -> slab[s], reduced in a fixed
+//    order by k_reduce_rows.  The three m-blocks of a slab are dispatched to
+//    the same XCD back to back, so the x rows they share come from its L2.
+//  * K tiles of 32 nodes, double-buffered in LDS as [row][node] f16 hi / lo
+//    (the MFMA operands are k-contiguous; dh' and x are node-major): each lane
+//    loads 4 consecutive columns of two adjacent nodes and writes (node 2p,
+//    node 2p + 1) pairs as dwords; the loads of the next two tiles are in
+//    flight during the MFMAs of the current one.
+//  * wave (wm, wn): m-tiles wm + 4 i (< 11), n-tiles wn + 2 j (< Fu / 16).
+constexpr int kGM = 176;   // dh' columns per block (kDH = 3 kGM)
+constexpr int kGK = 32;    // nodes per K tile
+constexpr int kGPt = 40;   // LDS row pitch in halves (80 B: 16-B aligned fragment reads)
+constexpr int kGMaxF = 256;
 
-template <typename TB>
-__global__ void __launch_bounds__(TW * 64) k_gemm_tn(const float* __restrict__ A, int64_t lda,
-                                                     const TB* __restrict__ B, int64_t ldb,
-                                                     int64_t M, int64_t N, int64_t K,
-                                                     int64_t k_per_split,
-                                                     float* __restrict__ slab) {
-  __shared__ float As[TK][TT + 4];
-  __shared__ float Bs[TK][TT + 4];
+size_t gw_smem(int Fu) { return size_t(2) * 2 * (kGM + Fu) * kGPt * sizeof(_Float16); }
+
+struct GwStage {  // one K tile in flight: 2 items x 2 nodes x 4 columns, per operand
+  f32x4 a[2][2], b[2][2];
+};
+
+__device__ __forceinline__ uint32_t pk_hi_lo(float v0, float v1, uint32_t& lo) {
+  typedef __fp16 h2 __attribute__((ext_vector_type(2)));
+  const h2 h = __builtin_amdgcn_cvt_pkrtz(v0, v1);
+  const h2 l = __builtin_amdgcn_cvt_pkrtz(v0 - float(h[0]), v1 - float(h[1]));
+  lo = *reinterpret_cast<const uint32_t*>(&l);
+  return *reinterpret_cast<const uint32_t*>(&h);
+}
+
+template <typename XT, bool VEC>
+__device__ __forceinline__ f32x4 gw_x4(const typename XT::T* __restrict__ x, int64_t ldx, int F,
+                                       int64_t r, int f0) {
+  const typename XT::T* p = x + r * ldx + f0;
+  if (VEC && f0 + 3 < F) return load4<XT>(p);
+  f32x4 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = f0 + q < F ? ldx1(p + q) : 0.f;
+  return v;
+}
+
+template <typename XT, bool VEC, int NJ>
+__global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
+                                            const typename XT::T* __restrict__ x, int64_t ldx,
+                                            int F, int Fu, int64_t N, int64_t kps, int S,
+                                            const uint32_t* __restrict__ amax,
+                                            float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int b = blockIdx.x, rem = b % 24;
+  const int mb = rem >> 3, s = (b / 24) * 8 + (rem & 7);
+  if (s >= S) return;  // block-uniform, before any barrier
+  const int64_t kb = int64_t(s) * kps, ke = min(N, kb + kps);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t m0 = int64_t(blockIdx.x) * TT, n0 = int64_t(blockIdx.y) * TT;
-  const int64_t kb = int64_t(blockIdx.z) * k_per_split;
-  const int64_t ke = min(K, kb + k_per_split);
-  f32x4 acc[TT / 16];
+  const int wm = wave & 3, wn = wave >> 2;
+  const int NTn = Fu >> 4, nB = 16 * (Fu >> 2);  // B items: 16 node pairs x Fu / 4 chunks
+  const int ea = scale_exp(__uint_as_float(amax[0])), eb = scale_exp(__uint_as_float(amax[1]));
+  const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
+  const float ua = ldexpf(1.0f, -ea), ub = ldexpf(1.0f, -eb);  // two steps: 2^-(ea+eb) may underflow
+  _Float16* buf = reinterpret_cast<_Float16*>(gsm);
+  const int bsz = 2 * (kGM + Fu) * kGPt;  // halves per buffer: A hi, A lo, B hi, B lo
+  auto Ahi = [&](int u) { return buf + u * bsz; };
+  auto Alo = [&](int u) { return buf + u * bsz + kGM * kGPt; };
+  auto Bhi = [&](int u) { return buf + u * bsz + 2 * kGM * kGPt; };
+  auto Blo = [&](int u) { return buf + u * bsz + 2 * kGM * kGPt + Fu * kGPt; };
+
+  GwStage stg[2];  // tiles t + 1 and t + 2 in flight during the MFMAs of tile t
+  auto load = [&](GwStage& st, int64_t k0) {
 #pragma unroll
-  for (int t = 0; t < TT / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t k0 = kb; k0 < ke; k0 += TK) {
-    for (int idx = tid; idx < TK * TT; idx += TW * 64) {
-      const int kk = idx / TT, mm = idx - kk * TT;
-      const int64_t gk = k0 + kk;
-      const bool kin = gk < ke;
-      As[kk][mm] = (kin && m0 + mm < M) ? A[gk * lda + m0 + mm] : 0.f;
-      Bs[kk][mm] = (kin && n0 + mm < N) ? ldx1(B + gk * ldb + n0 + mm) : 0.f;
-    }
-    __syncthreads();
+    for (int it = 0; it < 2; ++it) {
+      const int i = tid + 512 * it, p = i & 15, c = i >> 4;
 #pragma unroll
-    for (int kk = 0; kk < TK; kk += 4) {
-      const float a = As[kk + (lane >> 4)][wave * 16 + (lane & 15)];
-#pragma unroll
-      for (int t = 0; t < TT / 16; ++t) {
-        const float b = Bs[kk + (lane >> 4)][t * 16 + (lane & 15)];
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+      for (int e = 0; e < 2; ++e) {
+        const int64_t r = k0 + 2 * p + e;
+        const bool ok = r < ke;
+        st.a[it][e] = (ok && c < kGM / 4)
+                          ? *reinterpret_cast<const f32x4*>(dh + r * kDH + mb * kGM + 4 * c)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        st.b[it][e] = (ok && i < nB) ? gw_x4<XT, VEC>(x, ldx, F, r, 4 * c)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    __syncthreads();
-  }
-  float* Cz = slab + int64_t(blockIdx.z) * M * N;
+  };
+  auto store = [&](const GwStage& st, int u) {
+    uint32_t* ah = reinterpret_cast<uint32_t*>(Ahi(u));
+    uint32_t* al = reinterpret_cast<uint32_t*>(Alo(u));
+    uint32_t* bh = reinterpret_cast<uint32_t*>(Bhi(u));
+    uint32_t* bl = reinterpret_cast<uint32_t*>(Blo(u));
 #pragma unroll
-  for (int t = 0; t < TT / 16; ++t)
+    for (int it = 0; it < 2; ++it) {
+      const int i = tid + 512 * it, p = i & 15, c = i >> 4;
+      if (c < kGM / 4) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t gm = m0 + wave * 16 + (lane >> 4) * 4 + r;
-      const int64_t gn = n0 + t * 16 + (lane & 15);
-      if (gm < M && gn < N) Cz[gm * N + gn] = acc[t][r];
+        for (int q = 0; q < 4; ++q) {
+          uint32_t lo;
+          const uint32_t hi = pk_hi_lo(st.a[it][0][q] * sa, st.a[it][1][q] * sa, lo);
+          ah[((4 * c + q) * kGPt >> 1) + p] = hi;
+          al[((4 * c + q) * kGPt >> 1) + p] = lo;
+        }
+      }
+      if (i < nB) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t lo;
+          const uint32_t hi = pk_hi_lo(st.b[it][0][q] * sb, st.b[it][1][q] * sb, lo);
+          bh[((4 * c + q) * kGPt >> 1) + p] = hi;
+          bl[((4 * c + q) * kGPt >> 1) + p] = lo;
+        }
+      }
     }
+  };
+
+  f32x4 acc[3][NJ];  // NJ >= the wave's n-tile count (Fu / 32, rounded up)
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t T = (ke - kb + kGK - 1) / kGK;
+  load(stg[0], kb);
+  store(stg[0], 0);
+  if (T > 1) load(stg[1], kb + kGK);
+  if (T > 2) load(stg[0], kb + 2 * kGK);
+  __syncthreads();
+  const int fo = (lane & 15) * kGPt + 8 * (lane >> 4);  // fragment offset in a buffer
+  // iteration t (buffer u = t & 1; nxt = the registers holding tile t + 1)
+  auto step = [&](int64_t t, int u, GwStage& nxt) {
+    f16x8 a_hi[3], a_lo[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int mt = wm + 4 * i;
+      if (mt < kGM / 16) {
+        a_hi[i] = *reinterpret_cast<const f16x8*>(Ahi(u) + mt * 16 * kGPt + fo);
+        a_lo[i] = *reinterpret_cast<const f16x8*>(Alo(u) + mt * 16 * kGPt + fo);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nt = wn + 2 * j;
+      if (nt < NTn) {
+        const f16x8 b_hi = *reinterpret_cast<const f16x8*>(Bhi(u) + nt * 16 * kGPt + fo);
+        const f16x8 b_lo = *reinterpret_cast<const f16x8*>(Blo(u) + nt * 16 * kGPt + fo);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          if (wm + 4 * i < kGM / 16) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi[i], b_hi, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi[i], b_lo, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_lo[i], b_hi, acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // tile t + 1 (loaded two iterations ago) into the other buffer, whose last
+    // readers finished before the previous barrier; its registers then take
+    // tile t + 3
+    if (t + 1 < T) {
+      store(nxt, u ^ 1);
+      if (t + 3 < T) load(nxt, kb + (t + 3) * kGK);
+    }
+    __syncthreads();
+  };
+  for (int64_t t = 0; t < T; t += 2) {  // unrolled by two: static stage registers
+    step(t, 0, stg[1]);
+    if (t + 1 < T) step(t + 1, 1, stg[0]);
+  }
+  float* Cz = slab + int64_t(s) * kDH * F;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int mt = wm + 4 * i;
+    if (mt >= kGM / 16) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nt = wn + 2 * j;
+      const int n = nt * 16 + (lane & 15);
+      if (nt >= NTn || n >= F) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = mb * kGM + mt * 16 + 4 * (lane >> 4) + q;
+        Cz[int64_t(m) * F + n] = (acc[i][j][q] * ua) * ub;
+      }
+    }
+  }
 }
 
 // Generic strided GEMM (grad_x = dh W): Cm(m, n) = sum_k A(m, k) B(k, n),
@@ -652,6 +828,25 @@ __global__ void __launch_bounds__(256) k_reduce_rows(const float* __restrict__ p
   }
 }
 
+// out[c] = sum of part[r * cols + c] over r < rows for cols <= 64, one block of
+// 1024 threads: 16 row groups (r = g mod 16, ascending) then the groups in
+// order -- a fixed order, 16x the parallelism of k_reduce_rows' serial loop
+__global__ void __launch_bounds__(1024) k_reduce_few(const float* __restrict__ part, int64_t rows,
+                                                     int cols, float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < cols)
+    for (int64_t r = g; r < rows; r += 16) s += part[r * cols + c];
+  red[g][c] = s;
+  __syncthreads();
+  if (threadIdx.x < cols) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += red[k][c];
+    out[c] = t;
+  }
+}
+
 // column sums of a [n, 64] fp32 matrix: fixed-grid partials part[block][64]
 __global__ void __launch_bounds__(256) k_colsum64(const float* __restrict__ a, int64_t n,
                                                   float* __restrict__ part) {
@@ -680,8 +875,10 @@ __global__ void __launch_bounds__(256) k_att_grad(const float* __restrict__ W, i
   (which ? gad : gas)[hc] = acc;
 }
 
-int wsplits(int64_t N) {
-  int64_t s = N / 8192;
+// K slabs of the grad_W' GEMM: >= 512 nodes each, at most 512 slabs (3 blocks
+// per slab, one block per CU at a time)
+int gw_slabs(int64_t N) {
+  int64_t s = N / 512;
   if (s < 1) s = 1;
   if (s > 512) s = 512;
   return int(s);
@@ -690,7 +887,7 @@ int wsplits(int64_t N) {
 int kf_fu(int F) { return (F + 63) / 64; }
 
 struct BwdLayout {
-  size_t whdr, bhi, blo, dpre, alpha, dt, uhub, cpart, hadot, spart, dh, slab, gw, gbp;
+  size_t whdr, amax, bhi, blo, dpre, alpha, dt, uhub, cpart, hadot, spart, dh, slab, gw, gbp;
 };
 
 BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
@@ -701,6 +898,7 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
   const int64_t ch = chunks > 0 ? chunks : 0;
   auto take = [&](size_t bytes) { size_t o = align_up(s.off, 256); s.off = o + bytes; return o; };
   L.whdr = take(64);
+  L.amax = take(64);
   L.bhi = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
   L.blo = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
   L.dpre = take(sizeof(float) * size_t(M) * 8);
@@ -711,7 +909,7 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
   L.hadot = take(sizeof(float) * size_t(hubs > 0 ? hubs : 0) * 8);
   L.spart = take(sizeof(float) * size_t(src_chunks > 0 ? src_chunks : 0) * (HC + H));
   L.dh = take(sizeof(float) * size_t(N) * kDH);
-  L.slab = take(sizeof(float) * size_t(wsplits(N)) * kDH * F);
+  L.slab = take(sizeof(float) * size_t(gw_slabs(N)) * kDH * F);
   L.gw = take(sizeof(float) * size_t(kDH) * F);
   L.gbp = take(sizeof(float) * size_t(kRedBlocks) * 64);
   return L;
@@ -788,6 +986,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   const BwdLayout L = bwd_layout(N, M, F, hubs, chunks, schunks, sz);
   char* b = static_cast<char*>(ws);
   float* whdr = reinterpret_cast<float*>(b + L.whdr);
+  uint32_t* amax = reinterpret_cast<uint32_t*>(b + L.amax);
   uint4* bhi = reinterpret_cast<uint4*>(b + L.bhi);
   uint4* blo = reinterpret_cast<uint4*>(b + L.blo);
   float* dpre = reinterpret_cast<float*>(b + L.dpre);
@@ -818,9 +1017,10 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   {
     int64_t blocks = (N + 3) / 4;
     if (blocks > 16384) blocks = 16384;
-    k_bwd_src<<<unsigned(blocks), 256, 0, stream>>>(colptr, csc_dst, csc_eid, N,
-                                                    shubs > 0 ? src_plan->hub_rank : nullptr,
-                                                    alpha_d, dpre, dt, g, att_src, att_dst, dh);
+    GFD_HIP_CHECK(hipMemsetAsync(amax, 0, 2 * sizeof(uint32_t), stream));
+    k_bwd_src<XT><<<unsigned(blocks), 256, 0, stream>>>(
+        colptr, csc_dst, csc_eid, N, shubs > 0 ? src_plan->hub_rank : nullptr, alpha_d, dpre, dt,
+        g, att_src, att_dst, x, F, ldx, dh, amax);
     GFD_LAUNCH_CHECK();
     if (shubs > 0) {
       k_bwd_src_hub1<<<unsigned((schunks + 3) / 4), 256, 0, stream>>>(
@@ -829,18 +1029,24 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
       GFD_LAUNCH_CHECK();
       k_bwd_src_hub2<<<unsigned(shubs), 512, 0, stream>>>(spart, src_plan->hub_chunk_ptr,
                                                           src_plan->hub_dst, dt, att_src, att_dst,
-                                                          dh);
+                                                          dh, amax);
       GFD_LAUNCH_CHECK();
     }
   }
   // 4. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
   {
-    const int splits = wsplits(N);
-    int64_t kps = (N + splits - 1) / splits;
-    kps = (kps + TK - 1) / TK * TK;
+    int64_t kps = (N + gw_slabs(N) - 1) / gw_slabs(N);
+    kps = (kps + kGK - 1) / kGK * kGK;
     const int64_t z = (N + kps - 1) / kps;
-    dim3 grid(unsigned((kDH + TT - 1) / TT), unsigned((F + TT - 1) / TT), unsigned(z));
-    k_gemm_tn<typename XT::T><<<grid, TW * 64, 0, stream>>>(dh, kDH, x, ldx, kDH, F, N, kps, slab);
+    const int Fu16 = (F + 15) / 16 * 16;
+    const size_t smem = gw_smem(Fu16);
+    const bool vec = ldx % 4 == 0 &&
+                     reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
+    auto kern = Fu16 <= 192 ? (vec ? &k_gw<XT, true, 6> : &k_gw<XT, false, 6>)
+                            : (vec ? &k_gw<XT, true, 8> : &k_gw<XT, false, 8>);
+    if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
+    kern<<<unsigned(24 * ((z + 7) / 8)), 512, smem, stream>>>(dh, x, ldx, F, Fu16, N, kps, int(z),
+                                                               amax, slab);
     GFD_LAUNCH_CHECK();
     const int64_t cols = int64_t(kDH) * F;
     k_reduce_rows<<<unsigned((cols + 255) / 256), 256, 0, stream>>>(slab, z, cols, cols, gw, 1);
@@ -854,7 +1060,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   if (grad_bias) {
     k_colsum64<<<kRedBlocks, 256, 0, stream>>>(g, N, gbp);
     GFD_LAUNCH_CHECK();
-    k_reduce_rows<<<1, 64, 0, stream>>>(gbp, kRedBlocks, 64, 64, grad_bias, 1);
+    k_reduce_few<<<1, 1024, 0, stream>>>(gbp, kRedBlocks, 64, grad_bias);
     GFD_LAUNCH_CHECK();
   }
   // 6. grad_x = dh W  (A = dh [N, 512] at row stride 528, B = W [512, F])
