@@ -50,9 +50,12 @@ constexpr int kSWaves = 8;
 #ifndef GFD_LIGHT_AP
 #define GFD_LIGHT_AP 2
 #endif
+#ifndef GFD_GENERAL_AP
+#define GFD_GENERAL_AP 2
+#endif
 // A-fragment k-steps read ahead in the MFMA loop (general, light)
 template <bool LIGHT>
-constexpr int ap_of() { return LIGHT ? GFD_LIGHT_AP : 2; }
+constexpr int ap_of() { return LIGHT ? GFD_LIGHT_AP : GFD_GENERAL_AP; }
 
 struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm queue)
   int v;          // lanes 0..3: {row, e_begin, e_end, hub_rank}; lanes 8..15: sources of
