@@ -100,16 +100,9 @@ __device__ __forceinline__ float bwd_pass1(const void* __restrict__ x, int64_t l
     const int nk = min(8, e1 - b);
     float xv[8][KF];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
-          xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * k), ldx));
-#pragma unroll
-      for (int q = 0; q < KF; ++q) {
-        const int f = lane + 64 * q;
-        const float t = xcvt(xr[f < F ? f : F - 1]);
-        xv[k][q] = f < F ? t : 0.f;
-      }
-    }
+    for (int k = 0; k < 8; ++k)  // rows past the segment: empty descriptors, no traffic
+      row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * k), ldx), F, lane, k < nk,
+                       xv[k]);
     float sel = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -135,6 +128,133 @@ __device__ __forceinline__ float bwd_pass1(const void* __restrict__ x, int64_t l
     }
   }
   return sum_xor8_16_32(adot);
+}
+
+// A destination with at most 8 messages: passes 1 and 2 in one sweep (the
+// whole segment is one batch, so adot is known before anything is written):
+// dpre = alpha (dA - adot) leaky'(pre) and alpha~ written once; returns dt.
+template <typename XT, int KF>
+__device__ __forceinline__ float bwd_single(const void* __restrict__ x, int64_t ldx, int F,
+                                            const int32_t* __restrict__ col, int e0, int e1,
+                                            const float* __restrict__ st, float t_h, float m_h,
+                                            float inv_h, const float (&u)[H][KF], float slope,
+                                            float dp, uint64_t seed, float* __restrict__ dpre,
+                                            float* __restrict__ alpha_d) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  const int sig = (8 * h + kk) * 4;
+  const int e = e0 + kk;
+  const bool valid = e < e1;
+  const int j = col[valid ? e : e1 - 1];
+  const float pre = st[int64_t(j) * 16 + h] + t_h;
+  const float al = __expf(leaky(pre, slope) - m_h) * inv_h;
+  float keepf = 1.0f;
+  if (dp > 0.f)
+    keepf = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? 1.0f / (1.0f - dp) : 0.f;
+  const int nk = e1 - e0;
+  float xv[8][KF];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)  // rows past the segment: empty descriptors, no traffic
+    row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * k), ldx), F, lane, k < nk,
+                     xv[k]);
+  float sel = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k < nk) {
+      float v[8];
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        float sacc = u[hh][0] * xv[k][0];
+#pragma unroll
+        for (int q = 1; q < KF; ++q) sacc = fmaf(u[hh][q], xv[k][q], sacc);
+        v[hh] = sacc;
+      }
+      const float r = treduce8(v);
+      sel = (lane & 7) == k ? r : sel;
+    }
+  }
+  const float dA = __int_as_float(__builtin_amdgcn_ds_bpermute(sig, __float_as_int(sel))) * keepf;
+  const float adot = sum_xor8_16_32(valid ? al * dA : 0.f);
+  const float dd = valid ? al * (dA - adot) * (pre > 0.f ? 1.0f : slope) : 0.f;
+  if (valid) {
+    dpre[int64_t(e) * 8 + h] = dd;
+    alpha_d[int64_t(e) * 8 + h] = al * keepf;
+  }
+  return sum_xor8_16_32(dd);
+}
+
+// Both destinations of a wave with at most 8 messages each (the common case:
+// light, lone and most general rows): bwd_single for the two of them with
+// every load of both issued together -- two memory round trips per wave
+// instead of two per destination.  Writes dt for both.
+template <typename XT, int KF>
+__device__ __forceinline__ void bwd_pair(const void* __restrict__ x, int64_t ldx, int F,
+                                         const int32_t* __restrict__ col, const int4 (&dsc)[2],
+                                         const float* __restrict__ st,
+                                         const float* __restrict__ stats,
+                                         const float (&u)[2][H][KF], float slope, float dp,
+                                         uint64_t seed, float* __restrict__ dpre,
+                                         float* __restrict__ alpha_d, float* __restrict__ dt) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  const int sig = (8 * h + kk) * 4;
+  float t_h[2], m_h[2], l_h[2], pre[2];
+  int j[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {  // round trip 1: the destination's logits / stats, sources
+    const int64_t i = dsc[d].x;
+    t_h[d] = st[i * 16 + H + h];
+    m_h[d] = stats[i * 16 + h];
+    l_h[d] = stats[i * 16 + H + h];
+    const int e = dsc[d].y + kk;
+    j[d] = col[e < dsc[d].z ? e : dsc[d].z - 1];
+  }
+  float xv[2][8][KF];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {  // round trip 2: source logits and rows
+    const int nk = dsc[d].z - dsc[d].y;
+    pre[d] = st[int64_t(j[d]) * 16 + h] + t_h[d];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j[d], 8 * k), ldx), F, lane, k < nk,
+                       xv[d][k]);
+  }
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const int e0 = dsc[d].y, e1 = dsc[d].z, nk = e1 - e0;
+    const int e = e0 + kk;
+    const bool valid = e < e1;
+    const float al = __expf(leaky(pre[d], slope) - m_h[d]) * (1.0f / (l_h[d] + kSoftmaxEps));
+    float keepf = 1.0f;
+    if (dp > 0.f)
+      keepf = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? 1.0f / (1.0f - dp) : 0.f;
+    float sel = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < nk) {
+        float v[8];
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {
+          float sacc = u[d][hh][0] * xv[d][k][0];
+#pragma unroll
+          for (int q = 1; q < KF; ++q) sacc = fmaf(u[d][hh][q], xv[d][k][q], sacc);
+          v[hh] = sacc;
+        }
+        const float r = treduce8(v);
+        sel = (lane & 7) == k ? r : sel;
+      }
+    }
+    const float dA =
+        __int_as_float(__builtin_amdgcn_ds_bpermute(sig, __float_as_int(sel))) * keepf;
+    const float adot = sum_xor8_16_32(valid ? al * dA : 0.f);
+    const float dd = valid ? al * (dA - adot) * (pre[d] > 0.f ? 1.0f : slope) : 0.f;
+    if (valid) {
+      dpre[int64_t(e) * 8 + h] = dd;
+      alpha_d[int64_t(e) * 8 + h] = al * keepf;
+    }
+    const float dts = sum_xor8_16_32(dd);
+    if (lane < 8) dt[int64_t(dsc[d].x) * 8 + lane] = dts;
+  }
 }
 
 // Pass 2: dpre = alpha (dA - adot) leaky'(pre) in place; returns dt (head lane & 7).
@@ -235,6 +355,18 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
   const int lane = threadIdx.x & 63;
   const int w = wave_uniform(threadIdx.x >> 6);
   const int64_t base = int64_t(blockIdx.x) * kUT;
+  const int NT = Fu / 16;
+
+  // U tiles per wave per head group (Fu <= 64 KF).  W fragments are loaded
+  // per tile: issuing all of them up front (96 VGPRs) measured 14 % slower
+  constexpr int PM = (4 * 4 * KF + kUW - 1) / kUW;
+  auto wfrag = [&](int hg, int pi, int s, uint4& bh, uint4& bl) {
+    const int p = w + kUW * pi;
+    const int hl = p / NT, ct = p - hl * NT, h = 4 * hg + hl;
+    const int64_t fi = (int64_t(h * 2 + s) * NT + ct) * 64 + lane;
+    bh = bhi[fi];
+    bl = blo[fi];
+  };
 
   int4 dsc[2];
 #pragma unroll
@@ -263,19 +395,29 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
   __syncthreads();
 
   // U = G W (two head groups of 4), then each wave keeps its rows' u_i
-  const int NT = Fu / 16;
   float u[2][H][KF];
+#if defined(GFD_BWD_ABLATE) && GFD_BWD_ABLATE == 2  // diagnostic: message passes only
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+      for (int q = 0; q < KF; ++q) u[d][hh][q] = 1e-3f * float(lane + hh + q);
+#else
 #pragma unroll
   for (int hg = 0; hg < 2; ++hg) {
-    for (int p = w; p < 4 * NT; p += kUW) {
-      const int hl = p / NT, ct = p - hl * NT, h = 4 * hg + hl;
+#pragma unroll
+    for (int pi = 0; pi < PM; ++pi) {
+      const int p = w + kUW * pi;
+      if (p >= 4 * NT) break;  // wave-uniform
+      const int hl = p / NT, ct = p - hl * NT;
       f32x4 am[2], ax[2];
 #pragma unroll
       for (int rg = 0; rg < 2; ++rg) am[rg] = ax[rg] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int64_t fi = (int64_t(h * 2 + s) * NT + ct) * 64 + lane;
-        const uint4 bh = bhi[fi], bl = blo[fi];
+        uint4 bh, bl;
+        wfrag(hg, pi, s, bh, bl);
 #pragma unroll
         for (int rg = 0; rg < 2; ++rg) {
           const int ao = (16 * rg + (lane & 15)) * kGS + 32 * s + 8 * (lane >> 4);
@@ -304,9 +446,21 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
         }
     __syncthreads();
   }
+#endif
+#if defined(GFD_BWD_ABLATE) && GFD_BWD_ABLATE == 1  // diagnostic: U phase only
+  if (u[0][0][0] == 1.2345e-30f && u[1][H - 1][KF - 1] == 1.2345e-30f) dt[0] = 0.f;
+  return;
+#endif
 
   // messages of this wave's two destinations
   const int h = lane & 7;
+  if constexpr (KF <= 3) {  // (F > 192: the two row sets would spill)
+    if (dsc[0].x >= 0 && dsc[1].x >= 0 && dsc[0].w < 0 && dsc[1].w < 0 &&
+        dsc[0].z - dsc[0].y <= 8 && dsc[1].z - dsc[1].y <= 8) {  // wave-uniform
+      bwd_pair<XT, KF>(x, ldx, F, col, dsc, st, stats, u, slope, dp, seed, dpre, alpha_d, dt);
+      return;
+    }
+  }
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
     const int i = dsc[d].x;
@@ -325,9 +479,15 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
     const float t_h = st[int64_t(i) * 16 + H + h];
     const float m_h = stats[int64_t(i) * 16 + h];
     const float inv_h = 1.0f / (stats[int64_t(i) * 16 + H + h] + kSoftmaxEps);
-    const float adot = bwd_pass1<XT, KF>(x, ldx, F, col, dsc[d].y, dsc[d].z, st, t_h, m_h, inv_h,
-                                         u[d], slope, dp, seed, dpre, alpha_d);
-    const float dts = bwd_pass2(col, dsc[d].y, dsc[d].z, st, t_h, m_h, inv_h, adot, slope, dpre);
+    float dts;
+    if (dsc[d].z - dsc[d].y <= 8) {
+      dts = bwd_single<XT, KF>(x, ldx, F, col, dsc[d].y, dsc[d].z, st, t_h, m_h, inv_h, u[d],
+                               slope, dp, seed, dpre, alpha_d);
+    } else {
+      const float adot = bwd_pass1<XT, KF>(x, ldx, F, col, dsc[d].y, dsc[d].z, st, t_h, m_h,
+                                           inv_h, u[d], slope, dp, seed, dpre, alpha_d);
+      dts = bwd_pass2(col, dsc[d].y, dsc[d].z, st, t_h, m_h, inv_h, adot, slope, dpre);
+    }
     if (lane < 8) dt[int64_t(i) * 8 + lane] = dts;
   }
 }
