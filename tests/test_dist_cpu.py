@@ -41,6 +41,14 @@ def _logits(x, W, a_s, a_d):
     return torch.cat([(h * a_s).sum(-1), (h * a_d).sum(-1)], 1)
 
 
+def _store_path():
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="gfd_gloo_")
+    os.close(fd)
+    os.unlink(path)  # the FileStore creates it
+    return path
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -48,8 +56,9 @@ def _free_port():
 
 
 def _rank_main(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous: no TCP port to race for (a freed ephemeral port can be
+    # taken again before rank 0 binds it)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         ei, x, W, a_s, a_d, b = _problem()
         rowptr, col = csr_cpu(ei, N)
@@ -69,7 +78,7 @@ def _rank_main(rank, world, port, q):
 def test_sharded_forward_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = _store_path()
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()

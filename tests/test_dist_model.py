@@ -71,6 +71,14 @@ def _patch_oracle_stages(gdist, ei):
     gdist.shard_aggregate_ep = shard_aggregate_ep
 
 
+def _store_path():
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="gfd_gloo_")
+    os.close(fd)
+    os.unlink(path)  # the FileStore creates it
+    return path
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -84,8 +92,9 @@ def _rank_main(rank, world, port, q):
         if p not in sys.path:
             sys.path.insert(0, p)
     from gfd import dist as gdist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous: no TCP port to race for (a freed ephemeral port can be
+    # taken again before rank 0 binds it)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         ei, x, m = _problem()
         _patch_oracle_stages(gdist, ei)
@@ -103,7 +112,7 @@ def _rank_main(rank, world, port, q):
 def test_model_sharded_orchestration_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = _store_path()
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
