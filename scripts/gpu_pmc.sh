@@ -1,17 +1,18 @@
 #!/bin/bash
-# PMC passes over a short bench run (one rocprofv3 pass per counter group,
-# kernel trace only): HBM traffic (FETCH_SIZE, WRITE_SIZE) and SQ wave states.
-# usage: scripts/gpu_pmc.sh TAG [bench.py path] [bench args...]
+# HBM traffic of the bench's kernels: one rocprofv3 --pmc pass per counter
+# (FETCH_SIZE, WRITE_SIZE), kernel trace only, each under its own limit; then
+# fold them into profiles/pmc_summary.json (scripts/pmc_summary.py).
+# usage: scripts/gpu_pmc.sh TAG [bench args...]
 set -u
 cd "$(dirname "$0")/.."
 TAG=${1:-pmc}; shift || true
-BENCH=${1:-bench.py}; shift || true
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU"
 i=0
-for c in "FETCH_SIZE" "WRITE_SIZE" "$SQ"; do
+for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/${TAG}_p$i -o run -- python $BENCH --steps 3 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/${TAG}_p$i.log 2>&1
-  rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/${TAG}_p$i -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-legs "$@" > gpurun_out/${TAG}_p$i.log 2>&1
+  rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_p$i.log; exit $rc; }
 done
+python3 scripts/pmc_summary.py gpurun_out/${TAG}_p1 gpurun_out/${TAG}_p2 c4 10000000 50000000 166 1 "$TAG" > gpurun_out/${TAG}_summary.txt 2>&1
+rc=$?; cat gpurun_out/${TAG}_summary.txt; exit $rc

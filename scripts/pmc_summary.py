@@ -1,35 +1,54 @@
 #!/usr/bin/env python3
-"""Fold the rocprofv3 --pmc passes of scripts/gpu_pmc.sh into profiles/pmc_summary.json.
+"""Fold the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_pmc.sh
+into profiles/pmc_summary.json, per bench stage.
 
 Per kernel (averaged over its dispatches): FETCH_SIZE and WRITE_SIZE (KiB in the
 CSV), converted to bytes.  On gfx950 FETCH_SIZE tallies 128-B requests at 64 B
 (MI355X_MICROARCH.md § HBM), so ``fetch_bytes`` = 2 x the raw figure; WRITE_SIZE
-is exact.  ``hbm_bytes_per_launch`` = fetch_bytes + write_bytes of the tile
-kernel, keyed by the bench workload, which bench.py reports as roofline.traffic.
+is exact.  Each bench stage (bench.py ``kernels``) gets ``hbm_bytes_per_launch``
+= the sum over its kernels, keyed ``{config}:{stage}:N=..:E=..:F=..:world=..``;
+bench.py reports the dominant stage's figure as ``roofline.traffic``.
 
-usage: pmc_summary.py <gpurun_out dir> N E F world [tag]
+usage: pmc_summary.py <fetch pass dir> <write pass dir> CONFIG N E F WORLD [tag]
 """
-import csv
 import collections
+import csv
+import glob
 import json
 import os
 import sys
 
 
-def per_kernel(path):
+def per_kernel(d):
+    paths = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not paths:
+        raise SystemExit(f"no counter_collection.csv under {d}")
     acc = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(open(paths[0])):
         name = r["Kernel_Name"]
         short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+        short = short.replace("gfd::fwd::", "")
         acc[short].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def stage_of(k):
+    if k.startswith("k_stream<"):
+        return "light" if k.rstrip(">").rstrip().endswith("true") else "general"
+    if k.startswith(("k_hub_partial", "k_hub_fin")):
+        return "hubs"
+    if k.startswith(("k_logits_lone", "k_wmax", "k_pack_")):
+        return "pack+logits+lone"
+    if k.startswith("k_lone"):
+        return "lone"
+    return None
+
+
 def main():
-    d, N, E, F, world = sys.argv[1], *map(int, sys.argv[2:6])
-    tag = sys.argv[6] if len(sys.argv) > 6 else ""
-    fetch = per_kernel(os.path.join(d, "pmc_FETCH_SIZE", "run_counter_collection.csv"))
-    write = per_kernel(os.path.join(d, "pmc_WRITE_SIZE", "run_counter_collection.csv"))
+    fd, wd, config = sys.argv[1], sys.argv[2], sys.argv[3]
+    N, E, F, world = map(int, sys.argv[4:8])
+    tag = sys.argv[8] if len(sys.argv) > 8 else ""
+    fetch, write = per_kernel(fd), per_kernel(wd)
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out_path = os.path.join(repo, "profiles", "pmc_summary.json")
     try:
@@ -44,18 +63,23 @@ def main():
         wb = write[k] * 1024
         kernels[k] = {"fetch_size_kib_raw": fetch[k], "fetch_bytes": fb, "write_bytes": wb,
                       "hbm_bytes_per_launch": fb + wb}
-    # the tile stage is k_split + the k_stream launches (general + light tiles), or k_fused
-    tile = sorted(k for k in kernels if k.startswith(("k_stream", "k_fused", "k_persist", "k_split")))
-    entry = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (two passes) {tag}",
-             "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 128-B requests at 64 B)",
-             "kernels": kernels}
-    if tile:
-        entry["tile_kernel"] = " + ".join(tile)
-        entry["hbm_bytes_per_launch"] = sum(kernels[k]["hbm_bytes_per_launch"] for k in tile)
-    summary[f"tile:N={N}:E={E}:F={F}:world={world}"] = entry
+    stages = collections.defaultdict(list)
+    for k in kernels:
+        s = stage_of(k)
+        if s:
+            stages[s].append(k)
+    for s, ks in stages.items():
+        summary[f"{config}:{s}:N={N}:E={E}:F={F}:world={world}"] = {
+            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (two passes) {tag}",
+            "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 128-B requests at 64 B)",
+            "kernels": {k: kernels[k] for k in sorted(ks)},
+            "hbm_bytes_per_launch": sum(kernels[k]["hbm_bytes_per_launch"] for k in ks),
+        }
     json.dump(summary, open(out_path, "w"), indent=1, sort_keys=True)
     for k, v in kernels.items():
-        print(f"{k:28s} fetch {v['fetch_bytes'] / 1e9:8.3f} GB  write {v['write_bytes'] / 1e9:8.3f} GB")
+        print(f"{k:60s} fetch {v['fetch_bytes'] / 1e9:8.3f} GB  write {v['write_bytes'] / 1e9:8.3f} GB")
+    for s, ks in stages.items():
+        print(f"stage {s:18s} {sum(kernels[k]['hbm_bytes_per_launch'] for k in ks) / 1e9:8.3f} GB")
 
 
 if __name__ == "__main__":
