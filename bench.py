@@ -59,7 +59,7 @@ def parse(argv=None):
     p.add_argument("--gamma", type=float, default=2.1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-legs", action="store_true")
-    p.add_argument("--legs", default="c4bwd,c5,c1,c2,c3",
+    p.add_argument("--legs", default="c4bwd,sample,c5,c1,c2,c3,temporal,ingest",
                    help="comma list of legs run after the headline line (N = 1)")
     p.add_argument("--legs-only", action="store_true",
                    help="skip the C4 headline timing (development)")
@@ -399,6 +399,9 @@ def main():
         if "c4bwd" in want:
             log("[bench] leg C4 forward + backward ...")
             legs["c4_layer_fwd_bwd"] = bench_legs.c4_layer_fwd_bwd(s, dev)
+        if "sample" in want:
+            log("[bench] leg neighbour sampling on the C4 graph ...")
+            legs["neighbor_sampling"] = bench_legs.neighbor_sampling(s, dev)
         del s, layer
         torch.cuda.empty_cache()
         if "c5" in want:
@@ -410,7 +413,8 @@ def main():
                                                           "dtype", "config", "roofline",
                                                           "kernels", "layer")}
         for name, fn in (("c1", "c1_gat2_forward"), ("c2", "c2_gat3_train_step"),
-                         ("c3", "c3_tgn_49_steps")):
+                         ("c3", "c3_tgn_49_steps"), ("temporal", "temporal_snapshots"),
+                         ("ingest", "ingest_id_map")):
             if name in want:
                 log(f"[bench] leg {fn} ...")
                 legs[fn] = getattr(bench_legs, fn)(dev)

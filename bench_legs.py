@@ -13,6 +13,15 @@
   49 time-step snapshots, eval mode.
 * ``c4_layer_fwd_bwd``   -- the C4 layer-0 GATConv forward + backward (no
   grad_x: layer-0 features are data), the training cost at C4 scale.
+* ``temporal_snapshots`` -- SURVEY.md §8f rank 4: every time step's
+  create_temporal_subgraph (dataset.py:198-240) on the Elliptic-shaped graph,
+  one device pass vs the numpy restatement per step (oracle/temporal_ref.py).
+* ``ingest_id_map``     -- §8f rank 2: dataset.py:92-101's id -> index map and
+  edge filter on Elliptic-shaped ids (inputs resident on the device) vs the
+  reference's dict + per-edge loop restated in Python.
+* ``neighbor_sampling`` -- §8f rank 3: 2-hop uniform sampling (fanouts 10, 10;
+  1,024 seeds) on the C4 graph vs the oracle's restatement (oracle/sample_ref.py)
+  of the same draws on a bounded number of batches.
 
 Synthetic data only (gfd.synth; the Elliptic CSVs are not in the reference).
 """
@@ -148,3 +157,113 @@ def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2):
                         f"bias; no grad_x), N={g.num_nodes} E={E}", "unit": "edges/s",
             "value": E / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
             "forward_ms": fwd_med, "backward_ms": med - fwd_med}
+
+
+def temporal_snapshots(dev, steps=20, warmup=3, cpu_runs=3):
+    from gfd.temporal import temporal_snapshots as snap
+    from oracle.temporal_ref import temporal_subgraph_ref
+    d = _elliptic(dev)
+    N, E = d["N"], d["E"]
+    t0, t1 = (int(v) for v in torch.stack([d["time_step"].min(), d["time_step"].max()]).tolist())
+    med, mean = _time(lambda: snap(d["time_step"], d["edge_index"], N, t0, t1 - t0 + 1),
+                      steps, warmup)
+    ts, ei = d["time_step"].cpu().numpy(), d["edge_index"].cpu().numpy()
+    times = []
+    for _ in range(1 + cpu_runs):
+        c0 = time.perf_counter()
+        for t in range(t0, t1 + 1):
+            temporal_subgraph_ref(ts, ei, t)
+        times.append(time.perf_counter() - c0)
+    tt = sorted(times[1:])
+    return {"workload": f"all {t1 - t0 + 1} time-step snapshots (nodes, kept edges, local ids) "
+                        f"of the Elliptic-shaped graph N={N} E={E}", "unit": "edges/s",
+            "value": E / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
+            "cpu_baseline": {"value": E / tt[len(tt) // 2], "unit": "edges/s",
+                             "median_s": tt[len(tt) // 2], "runs": cpu_runs, "cores": 1,
+                             "kind": "port",
+                             "sample": "the whole graph: oracle temporal_subgraph_ref (numpy, "
+                                       "one call per step, as the reference loops over steps)"}}
+
+
+def ingest_id_map(dev, steps=20, warmup=3, seed=0):
+    from gfd import _lib
+    from gfd.graph import _ws
+    d = _elliptic(dev)
+    N, E = d["N"], d["E"]
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randperm(4 * N, generator=g)[:N].to(torch.int64) * 7 + 1000   # distinct tx ids
+    ei = d["edge_index"].cpu()
+    src_ids, dst_ids = ids[ei[0]].clone(), ids[ei[1]].clone()
+    unknown = torch.rand(E, generator=g) < 0.01                               # a few unknown ids
+    src_ids[unknown] = -5
+    ids_d, s_d, t_d = ids.to(dev), src_ids.to(dev), dst_ids.to(dev)
+    lib = _lib.load()
+    stream = _lib.stream_handle(dev)
+    sorted_ids = torch.empty(N, dtype=torch.int64, device=dev)
+    sorted_idx = torch.empty(N, dtype=torch.int32, device=dev)
+    out = torch.empty((2, E), dtype=torch.int64, device=dev)
+    kept = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws1 = _ws(lib.gfd_id_map_workspace_size(N), dev)
+    ws2 = _ws(lib.gfd_edges_from_ids_workspace_size(E), dev)
+
+    def run():
+        _lib.call("gfd_id_map_build", ids_d.data_ptr(), N, sorted_ids.data_ptr(),
+                  sorted_idx.data_ptr(), ws1.data_ptr(), ws1.numel(), stream)
+        _lib.call("gfd_edges_from_ids", sorted_ids.data_ptr(), sorted_idx.data_ptr(), N,
+                  s_d.data_ptr(), t_d.data_ptr(), E, out.data_ptr(), kept.data_ptr(),
+                  ws2.data_ptr(), ws2.numel(), stream)
+
+    med, mean = _time(run, steps, warmup)
+    # the reference's dict comprehension + per-edge membership loop (dataset.py:92-101)
+    idl, sl, tl = [str(v) for v in ids.tolist()], src_ids.tolist(), dst_ids.tolist()
+    c0 = time.perf_counter()
+    idx = {nid: i for i, nid in enumerate(idl)}
+    res = []
+    for a, b in zip(sl, tl):
+        sa, sb = str(a), str(b)
+        if sa in idx and sb in idx:
+            res.append([idx[sa], idx[sb]])
+    cpu_s = time.perf_counter() - c0
+    ok = int(kept.item()) == len(res)
+    return {"workload": f"id map ({N} transaction ids) + edge filter/remap ({E} edges, 1% unknown "
+                        f"ids), inputs resident on the device", "unit": "edges/s",
+            "value": E / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
+            "kept_edges_match_cpu": ok,
+            "cpu_baseline": {"value": E / cpu_s, "unit": "edges/s", "seconds": cpu_s, "cores": 1,
+                             "kind": "port",
+                             "sample": "the whole input: dict comprehension + per-edge membership "
+                                       "loop of dataset.py:92-101 (without the pandas iterrows "
+                                       "overhead, so a lower bound on the reference's time)"}}
+
+
+def neighbor_sampling(s, dev, steps=20, warmup=3, batch=1024, fanouts=(10, 10), cpu_batches=2):
+    from gfd.sampler import NeighborSampler
+    from oracle.sample_ref import sample_ref
+    g = s["graph"]
+    N = g.num_nodes
+    smp = NeighborSampler(g, N, list(fanouts), seed=3)
+    gen = torch.Generator(device=dev).manual_seed(5)
+    seed_sets = [torch.randint(0, N, (batch,), device=dev, generator=gen) for _ in range(8)]
+    k = [0]
+    edges = []
+
+    def one():
+        b = smp.sample(seed_sets[k[0] % len(seed_sets)], seed=k[0])
+        edges.append(b.edge_ptr[-1])
+        k[0] += 1
+
+    med, mean = _time(one, steps, warmup)
+    avg_e = sum(edges) / len(edges)
+    rowptr, col = g.rowptr.cpu().numpy(), g.col.cpu().numpy()
+    c0 = time.perf_counter()
+    for b in range(cpu_batches):
+        sample_ref(rowptr, col, seed_sets[b].cpu().numpy(), list(fanouts), b)
+    cpu_s = (time.perf_counter() - c0) / cpu_batches
+    return {"workload": f"2-hop uniform neighbour sampling (fanouts {list(fanouts)}, {batch} "
+                        f"seeds per batch, relabelled subgraph) on the C4 graph N={N}",
+            "unit": "sampled edges/s", "value": avg_e / (med * 1e-3), "ms_per_batch": med,
+            "ms_mean": mean, "sampled_edges_per_batch": avg_e,
+            "cpu_baseline": {"value": avg_e / cpu_s, "unit": "sampled edges/s",
+                             "seconds_per_batch": cpu_s, "cores": 1, "kind": "port",
+                             "sample": f"{cpu_batches} batches of the same seeds: "
+                                       f"oracle/sample_ref.py (pure Python Floyd draws)"}}
