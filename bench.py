@@ -119,6 +119,11 @@ class Layer:
         self.st = torch.empty((self.N, 2 * H), dtype=torch.float32, device=dev)
         rows = spec.node_hi - spec.node_lo
         self.st_local = torch.empty((max(rows, 1), 2 * H), dtype=torch.float32, device=dev)
+        # N > 1: the source-logit half of every node block is all-gathered
+        # (gfd.dist.exchange_logits: [N, 8] instead of [N, 16])
+        per = (self.N + world - 1) // world
+        self.s_local = torch.zeros((per, H), dtype=torch.float32, device=dev)
+        self.s_all = torch.empty((per * world, H), dtype=torch.float32, device=dev)
         self.out = torch.empty((max(self.n_dst, 1), C), dtype=torch.float32, device=dev)
         self.ws = torch.empty(self.lib.gfd_gat_fwd_workspace_size(
             self.N, self.n_dst, F, H, C, self.plan.num_hubs, self.plan.num_chunks),
@@ -147,14 +152,21 @@ class Layer:
                       self.packed.data_ptr(), H, C, self.st.data_ptr(), self.xmax.data_ptr(),
                       self.stream)
         else:
+            # gfd.dist.exchange_logits with persistent buffers: s of the node
+            # block all-gathered, [s | t] of the own destinations computed here
             import torch.distributed as dist
-            from gfd import dist as gdist
             rows = spec.node_hi - spec.node_lo
             if rows > 0:
                 _lib.call("gfd_gat_logits_ex", x[spec.node_lo:].data_ptr(), self.xdt, rows, F,
                           s["ldx"], self.packed.data_ptr(), H, C, self.st_local.data_ptr(),
                           self.xmax.data_ptr(), self.stream)
-            self.st.copy_(gdist.all_gather_rows(self.st_local[:rows], self.N, self.world))
+                self.s_local[:rows] = self.st_local[:rows, :H]
+            dist.all_gather_into_tensor(self.s_all, self.s_local)
+            self.st[:, :H] = self.s_all[:self.N]
+            if self.n_dst > 0:
+                _lib.call("gfd_gat_logits_ex", x[spec.dst_lo:].data_ptr(), self.xdt, self.n_dst,
+                          F, s["ldx"], self.packed.data_ptr(), H, C,
+                          self.st[spec.dst_lo:].data_ptr(), self.xmax.data_ptr(), self.stream)
             dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
 
     def aggregate(self, stages):

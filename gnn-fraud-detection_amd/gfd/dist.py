@@ -7,13 +7,14 @@ source-side data crosses GPUs.  Shards are contiguous destination ranges
 balanced by message count (prefix sum over in-degree).
 
 Layer 0 keeps ``x`` halo-resident (every rank holds the rows its in-edges
-reference; for a power-law graph that is nearly all of x).  The per-node
-attention logits are then computed for the rank's own destination block and
-exchanged with one RCCL all-gather of ``[N, 2H]`` fp32 (the "halo" of the
-north star: 64 B per node instead of the 664 B feature row), after which the
-fused aggregate-project kernel runs on the local shard with no further
-communication.  Hidden layers all-gather the previous layer's ``[N, 64]``
-output instead.
+reference; for a power-law graph that is nearly all of x).  Only the SOURCE
+logits s_j cross GPUs (``exchange_logits``): each rank computes ``[s | t]`` for
+an equal node block, all-gathers the s half (``[N, H]`` fp32: 32 B per node
+instead of the 664 B feature row -- the "halo" of the north star), and
+recomputes ``[s | t]`` for its own destination block, whose t it is the only
+reader of.  The fused aggregate-project kernels then run on the local shard
+with no further communication.  Hidden layers all-gather the previous layer's
+``[N, 64]`` output instead.
 """
 from __future__ import annotations
 
@@ -122,16 +123,56 @@ def shard_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
     """``[node_hi - node_lo, 16]`` attention logits (s | t) of this rank's node block.
     ``xmax`` (optional one-float device tensor) accumulates max |x| over the block
     (atomic max: start it at 0, reduce it over ranks before the aggregation)."""
+    return logits_rows(x, packed, spec.node_lo, spec.node_hi, xmax)
+
+
+def logits_rows(x: torch.Tensor, packed: torch.Tensor, lo: int, hi: int,
+                xmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``[hi - lo, 16]`` attention logits (s | t) of rows lo:hi of x
+    (gfd_gat_logits_ex); ``xmax`` (optional one-float device tensor)
+    accumulates max |x| over those rows (atomic max)."""
     from . import _lib
     from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
     H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
-    rows = spec.node_hi - spec.node_lo
-    st_local = torch.empty((rows, 2 * H), dtype=torch.float32, device=x.device)
-    if rows > 0:
-        _lib.call("gfd_gat_logits_ex", x[spec.node_lo:].data_ptr(), _lib.x_dtype_code(x), rows,
-                  x.size(1), x.stride(0), packed.data_ptr(), H, C, st_local.data_ptr(),
+    out = torch.empty((max(hi - lo, 0), 2 * H), dtype=torch.float32, device=x.device)
+    if hi > lo:
+        _lib.call("gfd_gat_logits_ex", x[lo:].data_ptr(), _lib.x_dtype_code(x), hi - lo,
+                  x.size(1), x.stride(0), packed.data_ptr(), H, C, out.data_ptr(),
                   _lib.ptr(xmax), _lib.stream_handle(x.device))
-    return st_local
+    return out
+
+
+def exchange_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
+                    xmax: Optional[torch.Tensor] = None, group=None,
+                    logits_fn=None) -> torch.Tensor:
+    """The ``[N, 16]`` logits table a shard's aggregation reads: s (columns
+    0..7) for every node, t (8..15) for the rank's destinations
+    ``dst_lo:dst_hi`` (other rows' t are never read and left unset).
+
+    s of the equal node block is all-gathered (one RCCL collective of
+    ``[N, 8]``: half the bytes of gathering [s | t]); [s | t] of the
+    destination block is then computed locally into its rows (its s
+    bit-identical to the gathered one: the same per-row arithmetic).
+    ``logits_fn(lo, hi)`` -> [hi - lo, 16] replaces the HIP logits (tests)."""
+    H = 8
+    N = x.size(0)
+    if logits_fn is None:
+        def logits_fn(lo, hi):
+            return logits_rows(x, packed, lo, hi, xmax)
+    if spec.world == 1:
+        return logits_fn(0, N)
+    import torch.distributed as dist
+    per = (N + spec.world - 1) // spec.world
+    blk = logits_fn(spec.node_lo, spec.node_hi)
+    s_local = torch.zeros((per, H), dtype=torch.float32, device=blk.device)
+    s_local[:blk.size(0)] = blk[:, :H]
+    s_all = torch.empty((per * spec.world, H), dtype=torch.float32, device=blk.device)
+    dist.all_gather_into_tensor(s_all, s_local, group=group)
+    st = torch.empty((N, 2 * H), dtype=torch.float32, device=blk.device)
+    st[:, :H] = s_all[:N]
+    if spec.dst_hi > spec.dst_lo:
+        st[spec.dst_lo:spec.dst_hi] = logits_fn(spec.dst_lo, spec.dst_hi)
+    return st
 
 
 def shard_aggregate(x: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tensor,
@@ -228,8 +269,8 @@ def shard_aggregate_ep(h: torch.Tensor, graph, st: torch.Tensor, packed: torch.T
 
 def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, residual: bool,
                           group=None) -> torch.Tensor:
-    """One layer body on this rank: logits of the rank's node block, RCCL
-    all-gather of the [N, 16] logits (and max|x|), the rank's destinations
+    """One layer body on this rank: source logits exchanged
+    (``exchange_logits``) and max|x| reduced, the rank's destinations
     aggregated with BN / ReLU / residual in the store.  ``h`` is the layer
     input for ALL N nodes (layer 0: the halo-resident features)."""
     import torch.distributed as dist
@@ -237,12 +278,9 @@ def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, res
     packed = pack_weights(conv.lin_src.weight.detach(), conv.att_src.detach(),
                           conv.att_dst.detach())
     xmax = torch.zeros(1, dtype=torch.float32, device=h.device)
-    st_local = shard_logits(h, packed, spec, xmax)
+    st = exchange_logits(h, packed, spec, xmax, group=group)
     if spec.world > 1:
-        st = all_gather_rows(st_local, h.size(0), spec.world, group=group)
         dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
-    else:
-        st = st_local
     res = None
     if residual:
         res = h[spec.dst_lo:spec.dst_hi]

@@ -65,11 +65,14 @@ def _rank_main(rank, world, port, q):
         spec = gdist.ShardSpec(rowptr, rank, world)
         st_local = _logits(x[spec.node_lo:spec.node_hi], W, a_s, a_d)
         st = gdist.all_gather_rows(st_local, N, world)
+        # the product exchange: s of every node gathered, [s | t] of the own destinations
+        st_x = gdist.exchange_logits(x, None, spec,
+                                     logits_fn=lambda lo, hi: _logits(x[lo:hi], W, a_s, a_d))
         out_local = ref.gatconv_forward_at(x, rowptr, col, torch.arange(spec.dst_lo, spec.dst_hi),
                                            W, a_s, a_d, b)
         out = gdist.all_gather_v_rows(out_local, spec.dst_bounds)
         if rank == 0:
-            q.put((st, out, spec.dst_bounds))
+            q.put((st, out, spec.dst_bounds, st_x, (spec.dst_lo, spec.dst_hi)))
     finally:
         dist.destroy_process_group()
 
@@ -82,12 +85,15 @@ def test_sharded_forward_matches_single_process(world):
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    st, out, bounds = q.get(timeout=120)
+    st, out, bounds, st_x, (d_lo, d_hi) = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     ei, x, W, a_s, a_d, b = _problem()
-    assert_close(st, _logits(x, W, a_s, a_d), what="gathered logits")
+    full_st = _logits(x, W, a_s, a_d)
+    assert_close(st, full_st, what="gathered logits")
+    assert_close(st_x[:, :H], full_st[:, :H], what="exchanged source logits")
+    assert_close(st_x[d_lo:d_hi], full_st[d_lo:d_hi], what="own destinations' [s | t]")
     full = ref.gatconv_forward(x, ei, W, a_s, a_d, b, heads=H)
     assert_close(out, full, what=f"sharded forward, world {world}")
     # the shards really are uneven in destinations but balanced in messages

@@ -48,11 +48,11 @@ def _patch_oracle_stages(gdist, ei):
     def pack_weights(W, a_s, a_d):
         return {"W": W, "a_s": a_s, "a_d": a_d}
 
-    def shard_logits(h, packed, spec, xmax=None):
-        hh = (h[spec.node_lo:spec.node_hi] @ packed["W"].t()).view(-1, H, C)
+    def logits_rows(h, packed, lo, hi, xmax=None):
+        hh = (h[lo:hi] @ packed["W"].t()).view(-1, H, C)
         a_s, a_d = packed["a_s"].view(1, H, C), packed["a_d"].view(1, H, C)
-        if xmax is not None and spec.node_hi > spec.node_lo:
-            xmax.copy_(torch.maximum(xmax, h[spec.node_lo:spec.node_hi].abs().max().view(1)))
+        if xmax is not None and hi > lo:
+            xmax.copy_(torch.maximum(xmax, h[lo:hi].abs().max().view(1)))
         return torch.cat([(hh * a_s).sum(-1), (hh * a_d).sum(-1)], 1)
 
     def shard_aggregate_ep(h, graph, st, packed, bias, spec, slope, xmax, scale_shift, relu,
@@ -67,7 +67,7 @@ def _patch_oracle_stages(gdist, ei):
         return y + residual if residual is not None else y
 
     gdist.pack_weights = pack_weights
-    gdist.shard_logits = shard_logits
+    gdist.logits_rows = logits_rows
     gdist.shard_aggregate_ep = shard_aggregate_ep
 
 
