@@ -90,4 +90,13 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t pos, uint32
 
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// max of non-negative floats into *dst (their bit patterns order like the
+// values).  Skips the atomic when *dst already holds at least v: thousands of
+// same-address atomics otherwise serialise in L2 (one per wave of a large grid).
+__device__ __forceinline__ void atomic_max_nonneg(float* dst, float v) {
+  unsigned int* p = reinterpret_cast<unsigned int*>(dst);
+  const unsigned int bits = __float_as_uint(v);
+  if (bits > __atomic_load_n(p, __ATOMIC_RELAXED)) atomicMax(p, bits);
+}
+
 }  // namespace gfd

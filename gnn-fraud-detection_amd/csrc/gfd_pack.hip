@@ -236,8 +236,7 @@ __global__ void __launch_bounds__(256) k_logits_s(const typename XT::T* __restri
   if (xmax) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
-    if (lane == 0)  // non-negative floats order like their bit patterns
-      atomicMax(reinterpret_cast<unsigned int*>(xmax), __float_as_uint(am));
+    if (lane == 0) atomic_max_nonneg(xmax, am);
   }
 }
 
@@ -273,7 +272,7 @@ __global__ void __launch_bounds__(256) k_logits_u(const typename XT::T* __restri
   if (xmax) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(xmax), __float_as_uint(am));
+    if (lane == 0) atomic_max_nonneg(xmax, am);
   }
 }
 
