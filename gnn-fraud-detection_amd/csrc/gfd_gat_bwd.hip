@@ -917,6 +917,84 @@ __global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
   }
 }
 
+// grad_x = dh W for F <= 64 (hidden layers) on f16 MFMA 16x16x32 with the
+// 3-term split: A = dh rows (k = the 512 head-channel columns, contiguous in a
+// row: no transpose), scaled by 2^ea from max |dh'| (k_bwd_src); B = the
+// k_bwd_msg W fragments (fragment (2h + s, ct) is k-step 2h + s of W[hC+c][f]),
+// resident in LDS for the launch.  One 16-row tile per wave at a time, the
+// next k-step's row loads in flight during the current k-step's MFMAs.
+constexpr int kGxNT = 4;  // F <= 64
+constexpr int kGxKS = HC / 32;
+
+__global__ void __launch_bounds__(512) k_gx(const float* __restrict__ dh, int64_t N, int F,
+                                            const uint4* __restrict__ bhi,
+                                            const uint4* __restrict__ blo,
+                                            const float* __restrict__ whdr,
+                                            const uint32_t* __restrict__ amax,
+                                            float* __restrict__ gx) {
+  __shared__ uint4 Bh[kGxKS][kGxNT][64], Bl[kGxKS][kGxNT][64];
+  const int NT = (F + 15) / 16;
+  for (int i = threadIdx.x; i < kGxKS * kGxNT * 64; i += blockDim.x) {
+    const int ks = i / (kGxNT * 64), ct = (i / 64) % kGxNT, l = i & 63;
+    const bool in = ct < NT;
+    const int64_t fi = (int64_t(ks) * NT + ct) * 64 + l;
+    Bh[ks][ct][l] = in ? bhi[fi] : make_uint4(0, 0, 0, 0);
+    Bl[ks][ct][l] = in ? blo[fi] : make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const int ea = scale_exp(__uint_as_float(amax[0]));
+  const float sa = ldexpf(1.0f, ea);
+  const float un = ldexpf(1.0f, -ea) * whdr[0];
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwave = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const int64_t tiles = (N + 15) / 16;
+  for (int64_t t = wave; t < tiles; t += nwave) {
+    const int64_t row = t * 16 + r;
+    const float* ar = dh + (row < N ? row : N - 1) * kDH + 8 * g;
+    f32x4 am[kGxNT], ax[kGxNT];
+#pragma unroll
+    for (int ct = 0; ct < kGxNT; ++ct) am[ct] = ax[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(ar), v1 = *reinterpret_cast<const f32x4*>(ar + 4);
+#pragma unroll
+    for (int ks = 0; ks < kGxKS; ++ks) {
+      union { f16x8 v; _Float16 e[8]; } hi, lo;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x = (q < 4 ? v0[q] : v1[q - 4]) * sa;
+        const _Float16 xh = (_Float16)x;
+        hi.e[q] = xh;
+        lo.e[q] = (_Float16)((x - (float)xh) * kLoScale);
+      }
+      if (ks + 1 < kGxKS) {
+        v0 = *reinterpret_cast<const f32x4*>(ar + 32 * (ks + 1));
+        v1 = *reinterpret_cast<const f32x4*>(ar + 32 * (ks + 1) + 4);
+      }
+#pragma unroll
+      for (int ct = 0; ct < kGxNT; ++ct) {
+        if (ct < NT) {
+          const uint4 bh = Bh[ks][ct][lane], bl = Bl[ks][ct][lane];
+          const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+          const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+          am[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, am[ct], 0, 0, 0);
+          ax[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, ax[ct], 0, 0, 0);
+          ax[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, ax[ct], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < kGxNT; ++ct) {
+      const int n = 16 * ct + r;
+      if (ct >= NT || n >= F) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t orow = t * 16 + 4 * g + q;
+        if (orow < N) gx[orow * F + n] = (am[ct][q] + ax[ct][q] * (1.0f / kLoScale)) * un;
+      }
+    }
+  }
+}
+
 // Generic strided GEMM (grad_x = dh W): Cm(m, n) = sum_k A(m, k) B(k, n),
 // X(r, c) = X[r * s_r + c * s_c]; 64x64 tile, BK = 16, 4 waves of 32x32.
 constexpr int GB = 64, GK = 16;
@@ -1225,7 +1303,12 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
     GFD_LAUNCH_CHECK();
   }
   // 6. grad_x = dh W  (A = dh [N, 512] at row stride 528, B = W [512, F])
-  if (grad_x) {
+  if (grad_x && F <= 16 * kGxNT) {
+    int64_t nb = ((N + 15) / 16 + 7) / 8;
+    if (nb > cu_count()) nb = cu_count();
+    k_gx<<<unsigned(nb), 512, 0, stream>>>(dh, N, F, bhi, blo, whdr, amax, grad_x);
+    GFD_LAUNCH_CHECK();
+  } else if (grad_x) {
     dim3 grid(unsigned((N + GB - 1) / GB), unsigned((F + GB - 1) / GB));
     k_gemm<<<grid, 256, 0, stream>>>(dh, kDH, 1, W, F, 1, grad_x, F, N, F, HC);
     GFD_LAUNCH_CHECK();
