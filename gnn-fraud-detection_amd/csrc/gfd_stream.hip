@@ -51,7 +51,7 @@ constexpr int kSWaves = 8;
 #define GFD_LIGHT_AP 2
 #endif
 #ifndef GFD_GENERAL_AP
-#define GFD_GENERAL_AP 2
+#define GFD_GENERAL_AP 1
 #endif
 // A-fragment k-steps read ahead in the MFMA loop (general, light)
 template <bool LIGHT>
