@@ -29,7 +29,7 @@ import torch
 from . import _lib
 
 HUB_THRESHOLD = int(os.environ.get("GFD_HUB_THRESHOLD", "128"))
-HUB_CHUNK = int(os.environ.get("GFD_HUB_CHUNK", "128"))
+HUB_CHUNK = int(os.environ.get("GFD_HUB_CHUNK", "256"))
 # source hubs of the backward's CSC pass (k_bwd_src chunks)
 SRC_HUB_THRESHOLD = 512
 SRC_HUB_CHUNK = 512
