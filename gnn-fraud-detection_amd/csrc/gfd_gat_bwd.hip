@@ -369,6 +369,7 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
   };
 
   int4 dsc[2];
+  bool need_u = false;  // a hub or a destination with more than its self loop
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
     const int64_t slot = base + w + 16 * d;
@@ -381,6 +382,28 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
         dsc[d] = make_int4(r, rowptr[r], rowptr[r + 1], hub_rank ? hub_rank[r] : -1);
       }
     }
+    need_u |= dsc[d].x >= 0 && (dsc[d].w >= 0 || dsc[d].z - dsc[d].y > 1);
+  }
+  // Only lone destinations (the self loop alone: alpha = 1, so dpre = alpha
+  // (dA - adot) = 0 and dt = 0 exactly, whatever u is): no U, no gathers.
+  // The plan's degree order puts them in the last blocks.
+  if (!__syncthreads_or(need_u)) {
+    const int h = lane & 7;
+    const float keep = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      if (dsc[d].x < 0 || lane >= 8) continue;
+      const int e = dsc[d].y;
+      float keepf = 1.0f;
+      if (dp > 0.f) keepf = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? keep : 0.f;
+      dpre[int64_t(e) * 8 + h] = 0.f;
+      alpha_d[int64_t(e) * 8 + h] = keepf;
+      dt[int64_t(dsc[d].x) * 8 + h] = 0.f;
+    }
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
     // G row: power-of-two scaled, fp16 hi / lo'
     const int i = dsc[d].x;
     const float gv = i >= 0 ? g[int64_t(i) * C + lane] : 0.f;
