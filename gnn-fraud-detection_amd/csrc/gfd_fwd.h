@@ -34,7 +34,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 struct PackLayout {
   int F, Fp, Fu, KP, KS, KB;
   size_t hdr_off, uv_off, whi_off, wlo_off, wsh_off, wsl_off, wbh_off, wbl_off, wph_off, wpl_off,
-      bytes;
+      uph_off, upl_off, bytes;
 };
 
 inline PackLayout pack_layout(int F) {
@@ -61,15 +61,21 @@ inline PackLayout pack_layout(int F) {
   // lane group g holds features 32 t + 4 g .. +3 and 32 t + 16 + 4 g .. +3
   L.wph_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 4 * 64, 256);
   L.wpl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 4 * 64, 256);
+  // the 2H logit vectors [U | V] as f16 hi / lo B fragments (one 16-column
+  // tile) in the same lane order (k_logits_lone's logits on f16 MFMA)
+  L.uph_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
+  L.upl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
   L.bytes = o;
   return L;
 }
 
-struct PackHeader {    // device-side, written by k_wmax
+struct PackHeader {    // device-side, written by k_wmax (uv_*: k_pack_uv_perm)
   float w_unscale;     // 2^-kw   (W / H fragments scaled by 2^kw)
   float w_scale;       // 2^kw
   float wb_unscale;    // 2^-kb   (Wbar fragments scaled by 2^kb)
   float wb_scale;      // 2^kb
+  float uv_unscale;    // 2^-ku   ([U | V] fragments scaled by 2^ku)
+  float uv_scale;      // 2^ku
 };
 
 // ---------------------------------------------------------------------------

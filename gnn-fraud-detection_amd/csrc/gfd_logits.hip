@@ -13,13 +13,14 @@
 // k_logits_lone: 8-wave blocks, two per CU, grid-stride over 16-row tiles.
 //   * lane (r = l & 15, g = l >> 4) loads features 16 s + 4 g .. +3 of row r
 //     for every fp32 k-step s (16-B loads, all issued before the first MFMA);
-//   * st = x . [U | V] on v_mfma_f32_16x16x4_f32 (exact fp32 chains, the same
-//     arithmetic as k_logits_s) with the folded logit vectors in LDS;
-//   * if any row of the tile is lone: the row scaled by 2^e (max |x| ->
-//     [2^13, 2^14)), split into f16 hi / lo', and out = x . Wbar^T on
-//     v_mfma_f32_16x16x32_f16 -- f16 k-step t is exactly fp32 k-steps 2t and
-//     2t+1 of the lane, matched by the permuted Wbar fragments (k_pack_wbar_perm)
-//     that stay in LDS for the launch;
+//   * the row, scaled by 2^e (max |x| -> [2^13, 2^14)), is split into f16
+//     hi / lo' once per f16 k-step t (fp32 k-steps 2 t and 2 t + 1 of the
+//     lane, matched by the permuted fragments of k_pack_wbar_perm /
+//     k_pack_uv_perm, which stay in LDS for the launch);
+//   * st = x . [U | V] on v_mfma_f32_16x16x32_f16 (3-term split, ~2^-21
+//     relative: 18 MFMAs per tile instead of 44 fp32 16x16x4 ones);
+//   * if any row of the tile is lone: out = x . Wbar^T from the same
+//     fragments (12 more MFMAs per k-step);
 //   * out rows (and, in training, the softmax stats: max = leaky(s_i + t_i),
 //     denominator 1) are written for lone rows only.
 #include "gfd_fwd.h"
@@ -39,13 +40,13 @@ template <typename XT, int KS>
 __global__ void __launch_bounds__(kLLWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_logits_lone(
     const typename XT::T* __restrict__ x, int64_t rows, int F, int64_t ldx,
-    const float* __restrict__ uv, int Fu, const PackHeader* __restrict__ hdr,
-    const uint4* __restrict__ wph, const uint4* __restrict__ wpl,
+    const PackHeader* __restrict__ hdr, const uint4* __restrict__ uph,
+    const uint4* __restrict__ upl, const uint4* __restrict__ wph, const uint4* __restrict__ wpl,
     const int32_t* __restrict__ rowptr, const float* __restrict__ bias, float slope,
     float* __restrict__ st, float* __restrict__ xmax, float* __restrict__ out,
     float* __restrict__ stats, Epi ep) {
   __shared__ uint4 WB[2][kLKB][4][64];  // permuted Wbar hi / lo fragments, zero past KB
-  __shared__ f32x4 UV[kLKS][64];        // logit vectors in the B layout of each k-step
+  __shared__ uint4 UP[2][kLKB][64];     // permuted [U | V] hi / lo fragments, zero past KB
   const int KB = (F + 31) / 32;
   const int kst = (F + 15) / 16;  // fp32 k-steps incl. the ragged tail
   const int ksf = F / 16;         // fp32 k-steps fully inside the row
@@ -54,15 +55,16 @@ k_logits_lone(
     WB[0][0][0][i] = in ? wph[i] : make_uint4(0, 0, 0, 0);
     WB[1][0][0][i] = in ? wpl[i] : make_uint4(0, 0, 0, 0);
   }
-  for (int i = threadIdx.x; i < kLKS * 64; i += blockDim.x) {
-    const int s = i >> 6, l = i & 63;
-    UV[s][l] = s < kst ? *reinterpret_cast<const f32x4*>(uv + (l & 15) * Fu + 16 * s + 4 * (l >> 4))
-                       : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = threadIdx.x; i < kLKB * 64; i += blockDim.x) {
+    const bool in = i < KB * 64;
+    UP[0][0][i] = in ? uph[i] : make_uint4(0, 0, 0, 0);
+    UP[1][0][i] = in ? upl[i] : make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int rl = lane & 15, g = lane >> 4;
   const float wbu = hdr->wb_unscale;
+  const float uvu = hdr->uv_unscale;
   float am = 0.f;  // max |x| over the values this lane loaded
   const int64_t wave = int64_t(blockIdx.x) * kLLWaves + (threadIdx.x >> 6);
   const int64_t nwave = int64_t(gridDim.x) * kLLWaves;
@@ -88,33 +90,21 @@ k_logits_lone(
       }
     }
     const bool lone = rin && rowptr[row + 1] - rowptr[row] == 1;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (s < kst) {
-        const f32x4 b = UV[s][lane];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][u], b[u], acc, 0, 0, 0);
-      }
-    }
     float rm = 0.f;  // max |x| of this lane's part of the row
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       rm = fmaxf(fmaxf(rm, fmaxf(fabsf(a[s].x), fabsf(a[s].y))), fmaxf(fabsf(a[s].z), fabsf(a[s].w)));
     am = fmaxf(am, rm);  // clamped tail rows repeat row rows - 1: harmless for a max
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t orow = t * 16 + 4 * g + r;
-      if (orow < rows) st[orow * 16 + rl] = acc[r];
-    }
-    if (__ballot(lone) == 0) continue;  // wave-uniform: no lone row in this tile
+    const bool any_lone = __ballot(lone) != 0;  // wave-uniform
     const int er = scale_exp(max_xor16_32(rm));  // lanes r, r + 16, r + 32, r + 48
     const float rs = ldexpf(1.0f, er);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     f32x4 o[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tt = 0; tt < kLKB; ++tt) {
+      if (tt >= KB) break;  // uniform: past the row's k-steps
       union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -123,26 +113,48 @@ k_logits_lone(
         hi.p[i] = __builtin_convertvector(v, f16x2);
         lo.u[i] = split_lo(v, hi.u[i]);
       }
+      {
+        const uint4 uh = UP[0][tt][lane], ul = UP[1][tt][lane];
+        const f16x8 u_h = *reinterpret_cast<const f16x8*>(&uh);
+        const f16x8 u_l = *reinterpret_cast<const f16x8*>(&ul);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_h, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_l, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, u_h, acc, 0, 0, 0);
+      }
+      if (any_lone) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
-        const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
-        const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
-        o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, o[ct], 0, 0, 0);
-        o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, o[ct], 0, 0, 0);
-        o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, o[ct], 0, 0, 0);
+        for (int ct = 0; ct < 4; ++ct) {
+          const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
+          const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+          const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, o[ct], 0, 0, 0);
+          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, o[ct], 0, 0, 0);
+          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, o[ct], 0, 0, 0);
+        }
       }
     }
-    // o[ct] element q of lane l: row 4 g + q, column 16 ct + rl
-    const float uns = ldexpf(1.0f, -er) * wbu;
+    // acc / o[ct] element q of lane l: row 4 g + q, column rl (16 ct + rl);
+    // the row's unscale comes from a lane holding that row
+    const float ers = ldexpf(1.0f, -er);
+    float sv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int src = 4 * g + q;
+      const float eq = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers)));
+      sv[q] = acc[q] * (eq * uvu);
+      const int64_t orow = t * 16 + src;
+      if (orow < rows) st[orow * 16 + rl] = sv[q];
+    }
+    if (!any_lone) continue;
     const int lone_i = lone ? 1 : 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int src = 4 * g + q;  // a lane holding row src's flag and scale
       const int lq = __builtin_amdgcn_ds_bpermute(src << 2, lone_i);
-      const float uq = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(uns)));
+      const float uq =
+          __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers))) * wbu;
       // the row's t logits (columns 8..15) next to its s logits (0..7)
-      const float tq = dpp_mov<0x128>(acc[q]);  // row_ror:8 within the 16-lane row
+      const float tq = dpp_mov<0x128>(sv[q]);  // row_ror:8 within the 16-lane row
       if (lq) {
         const int64_t orow = t * 16 + src;
 #pragma unroll
@@ -150,7 +162,7 @@ k_logits_lone(
           out[orow * C + ct * 16 + rl] =
               epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl, orow, ep);
         if (__builtin_expect(stats != nullptr, 0) && rl < H) {  // training (no dropout) only
-          stats[orow * 16 + rl] = leaky(acc[q] + tq, slope);
+          stats[orow * 16 + rl] = leaky(sv[q] + tq, slope);
           stats[orow * 16 + H + rl] = 1.0f;
         }
       }
@@ -175,8 +187,9 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
   auto kern = F <= 176 ? &k_logits_lone<XT, 11> : &k_logits_lone<XT, 12>;
   kern<<<int(nb), kLLWaves * 64, 0, stream>>>(
       static_cast<const typename XT::T*>(x), rows, F, ldx,
-      reinterpret_cast<const float*>(packed + L.uv_off), L.Fu,
       reinterpret_cast<const PackHeader*>(packed + L.hdr_off),
+      reinterpret_cast<const uint4*>(packed + L.uph_off),
+      reinterpret_cast<const uint4*>(packed + L.upl_off),
       reinterpret_cast<const uint4*>(packed + L.wph_off),
       reinterpret_cast<const uint4*>(packed + L.wpl_off), rowptr, bias, slope, st, xmax, out,
       stats, ep);

@@ -169,6 +169,46 @@ __global__ void k_pack_wbar_perm(const float* __restrict__ W, int F, int KB,
   wpl[idx] = lo.v;
 }
 
+// [U | V] fragments in the same lane order as k_pack_wbar_perm (one 16-column
+// tile: column n = q of uv, K = features), power-of-two scaled by max |uv| ->
+// [2^13, 2^14), f16 hi / lo.  One block: the max, then the fragments.
+__global__ void __launch_bounds__(256) k_pack_uv_perm(const float* __restrict__ uv, int F, int Fu,
+                                                      int KB, PackHeader* __restrict__ hdr,
+                                                      uint4* __restrict__ uph,
+                                                      uint4* __restrict__ upl) {
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  float m = 0.f;
+  for (int i = t; i < 2 * H * Fu; i += 256) m = fmaxf(m, fabsf(uv[i]));
+  red[t] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) red[t] = fmaxf(red[t], red[t + s]);
+    __syncthreads();
+  }
+  const int ku = scale_exp(red[0]);
+  const float sc = ldexpf(1.0f, ku);
+  if (t == 0) {
+    hdr->uv_scale = sc;
+    hdr->uv_unscale = ldexpf(1.0f, -ku);
+  }
+  for (int idx = t; idx < KB * 64; idx += 256) {  // (k-step, lane)
+    const int lane = idx & 63, kt = idx >> 6;
+    const int n = lane & 15, g = lane >> 4;
+    union { uint4 v; _Float16 h[8]; } hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 32 * kt + 4 * g + j + (j >= 4 ? 12 : 0);
+      const float v = f < F ? uv[n * Fu + f] * sc : 0.f;
+      const _Float16 hv = (_Float16)v;
+      hi.h[j] = hv;
+      lo.h[j] = (_Float16)(v - (float)hv);
+    }
+    uph[idx] = hi.v;
+    upl[idx] = lo.v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // st[r][q] = sum_f x[r][f] * uv[q][f] (q < 2H) on v_mfma_f32_16x16x4_f32 with the
 // 2H logit vectors stationary in registers (KSM k-steps of 16 features) and
@@ -357,6 +397,10 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   k_pack_wbar_perm<<<(n_wb + 255) / 256, 256, 0, stream>>>(
       weight, F, L.KB, hdr, reinterpret_cast<uint4*>(p + L.wph_off),
       reinterpret_cast<uint4*>(p + L.wpl_off));
+  GFD_LAUNCH_CHECK();
+  k_pack_uv_perm<<<1, 256, 0, stream>>>(reinterpret_cast<const float*>(p + L.uv_off), F, L.Fu,
+                                        L.KB, hdr, reinterpret_cast<uint4*>(p + L.uph_off),
+                                        reinterpret_cast<uint4*>(p + L.upl_off));
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
