@@ -361,10 +361,22 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
 #pragma unroll
     for (int q = 0; q < KF; ++q) acc[hh][q] = 0.f;
   float m = -INFINITY, l = 0.f;
+  // sources through 64-wide windows of col (lane i = message wb + i), the
+  // next window loaded one window ahead: a batch's logits and rows are one
+  // memory round trip, not a col -> (st, rows) chain of two (clamped: every
+  // load is in bounds)
+  int wb = e0;
+  int cw = col[min(e0 + lane, e1 - 1)];
+  int cn = col[min(e0 + 64 + lane, e1 - 1)];
   for (int b = e0; b < e1; b += 8) {
+    if (b - wb == 64) {
+      wb = b;
+      cw = cn;
+      cn = col[min(b + 64 + lane, e1 - 1)];
+    }
     const int e = b + kk;
     const bool valid = e < e1;
-    const int j = col[valid ? e : e1 - 1];  // clamped: every load is in bounds
+    const int j = __builtin_amdgcn_ds_bpermute((b - wb + kk) << 2, cw);
     const float v = leaky(st[int64_t(j) * 16 + h] + t_h, slope);
     const float mn = fmaxf(m, max_xor8_16_32(valid ? v : -INFINITY));
     const float sc = __expf(m - mn);  // 0 on the first batch, 1 while the max holds
@@ -387,7 +399,7 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
-          xrow<XT>(x, __builtin_amdgcn_readlane(j, 8 * k), ldx));
+          xrow<XT>(x, __builtin_amdgcn_readlane(cw, b - wb + k), ldx));
 #pragma unroll
       for (int q = 0; q < KF; ++q) {
         const int f = lane + 64 * q;

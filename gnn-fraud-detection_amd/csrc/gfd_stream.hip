@@ -118,9 +118,12 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF>& q,
     }
     if (lane == 0) ring->d = make_int4(p.live ? row : -1, e0, e1, hw);
   } else {
+    // messages past the slot's end (light slots of 2 or 3 messages; the
+    // padding sources repeat the last one) fetch nothing and read zeros
     constexpr int k = PART - 1;
     const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
-    row_regs<XT, KF>(xrow<XT>(x, jk, ldx), F, lane, true, q.xv[k]);
+    const int n = __builtin_amdgcn_readlane(p.v, 2) - __builtin_amdgcn_readlane(p.v, 1);
+    row_regs<XT, KF>(xrow<XT>(x, jk, ldx), F, lane, k < n, q.xv[k]);
   }
 }
 
