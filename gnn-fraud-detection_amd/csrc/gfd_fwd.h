@@ -362,22 +362,42 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
     for (int q = 0; q < KF; ++q) acc[hh][q] = 0.f;
   float m = -INFINITY, l = 0.f;
   // sources through 64-wide windows of col (lane i = message wb + i), the
-  // next window loaded one window ahead: a batch's logits and rows are one
-  // memory round trip, not a col -> (st, rows) chain of two (clamped: every
-  // load is in bounds)
+  // next window loaded one window ahead, so a batch's logits and rows are one
+  // memory round trip; and batch b + 8 is issued before batch b is consumed
+  // (two batches of rows in flight per wave).  Clamped: every load is in
+  // bounds; the issue past the last batch fetches rows of message e1 - 1.
   int wb = e0;
   int cw = col[min(e0 + lane, e1 - 1)];
   int cn = col[min(e0 + 64 + lane, e1 - 1)];
-  for (int b = e0; b < e1; b += 8) {
+  auto issue = [&](int b, float& sv, float (&xv)[8][KF]) {
     if (b - wb == 64) {
       wb = b;
       cw = cn;
       cn = col[min(b + 64 + lane, e1 - 1)];
     }
+    const int j = __builtin_amdgcn_ds_bpermute((b - wb + kk) << 2, cw);
+    sv = st[int64_t(j) * 16 + h];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // plain loads, f >= F reads x[F - 1] and selects 0: never the row padding
+      const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
+          xrow<XT>(x, __builtin_amdgcn_readlane(cw, b - wb + k), ldx));
+#pragma unroll
+      for (int q = 0; q < KF; ++q) {
+        const int f = lane + 64 * q;
+        const float t = xcvt(xr[f < F ? f : F - 1]);
+        xv[k][q] = f < F ? t : 0.f;
+      }
+    }
+  };
+  float sv, xv[8][KF];
+  issue(e0, sv, xv);
+  for (int b = e0; b < e1; b += 8) {
+    float sn, xn[8][KF];
+    issue(b + 8, sn, xn);
     const int e = b + kk;
     const bool valid = e < e1;
-    const int j = __builtin_amdgcn_ds_bpermute((b - wb + kk) << 2, cw);
-    const float v = leaky(st[int64_t(j) * 16 + h] + t_h, slope);
+    const float v = leaky(sv + t_h, slope);
     const float mn = fmaxf(m, max_xor8_16_32(valid ? v : -INFINITY));
     const float sc = __expf(m - mn);  // 0 on the first batch, 1 while the max holds
     float p = valid ? __expf(v - mn) : 0.f;
@@ -392,21 +412,7 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
     }
     m = mn;
     if (dp > 0.f) p = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? p * keep_scale : 0.f;
-    // all 8 rows of the batch issued together; clamped plain loads (f >= F
-    // reads x[F - 1] and selects 0: never the row padding)
     const int nk = min(8, e1 - b);
-    float xv[8][KF];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const typename XT::T* xr = reinterpret_cast<const typename XT::T*>(
-          xrow<XT>(x, __builtin_amdgcn_readlane(cw, b - wb + k), ldx));
-#pragma unroll
-      for (int q = 0; q < KF; ++q) {
-        const int f = lane + 64 * q;
-        const float t = xcvt(xr[f < F ? f : F - 1]);
-        xv[k][q] = f < F ? t : 0.f;
-      }
-    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (k < nk) {
@@ -420,6 +426,11 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
         }
       }
     }
+    sv = sn;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int q = 0; q < KF; ++q) xv[k][q] = xn[k][q];
   }
   return {m, sum_xor8_16_32(l)};
 }

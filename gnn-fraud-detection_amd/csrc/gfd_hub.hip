@@ -14,9 +14,9 @@ using namespace gfd::fwd;
 
 namespace {
 
-// five waves per SIMD (<= 96 VGPRs at KF = 3): one batch of 8 rows in flight each
+// four waves per SIMD (<= 128 VGPRs at KF = 3), two batches of 8 rows in flight each
 template <typename XT, int KF>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_hub_partial(
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_hub_partial(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t dst_offset, const float* __restrict__ st, float slope, float dp, uint64_t seed,
     const int4* __restrict__ chunks, int64_t num_chunks, float* __restrict__ part) {
