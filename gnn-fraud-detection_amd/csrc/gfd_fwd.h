@@ -34,7 +34,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 struct PackLayout {
   int F, Fp, Fu, KP, KS, KB;
   size_t hdr_off, uv_off, whi_off, wlo_off, wsh_off, wsl_off, wbh_off, wbl_off, wph_off, wpl_off,
-      uph_off, upl_off, bytes;
+      uph_off, upl_off, ush_off, usl_off, bytes;
 };
 
 inline PackLayout pack_layout(int F) {
@@ -65,6 +65,10 @@ inline PackLayout pack_layout(int F) {
   // tile) in the same lane order (k_logits_lone's logits on f16 MFMA)
   L.uph_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
   L.upl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
+  // ... and in the plain order (lane group g of k-step t: features 32 t + 8 g
+  // .. +7, the bf16 logits pass's 16-B loads)
+  L.ush_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
+  L.usl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
   L.bytes = o;
   return L;
 }

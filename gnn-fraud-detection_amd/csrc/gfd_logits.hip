@@ -12,7 +12,8 @@
 //
 // k_logits_lone: 8-wave blocks, two per CU, grid-stride over 16-row tiles.
 //   * lane (r = l & 15, g = l >> 4) loads features 16 s + 4 g .. +3 of row r
-//     for every fp32 k-step s (16-B loads, all issued before the first MFMA);
+//     for every fp32 k-step s (fp32), or 32 t + 8 g .. +7 for every f16
+//     k-step t (bf16) -- 16-B loads, all issued before the first MFMA;
 //   * the row, scaled by 2^e (max |x| -> [2^13, 2^14)), is split into f16
 //     hi / lo' once per f16 k-step t (fp32 k-steps 2 t and 2 t + 1 of the
 //     lane, matched by the permuted fragments of k_pack_wbar_perm /
@@ -72,28 +73,58 @@ k_logits_lone(
   for (int64_t t = wave; t < tiles; t += nwave) {
     const int64_t row = t * 16 + rl;
     const bool rin = row < rows;
-    const typename XT::T* xr = x + (rin ? row : rows - 1) * ldx + 4 * g;
-    f32x4 a[kLKS];
+    // fp32: lane group g holds features 16 s + 4 g .. +3 of fp32 k-step s (the
+    // permuted fragment order); bf16: features 32 t + 8 g .. +7 of f16 k-step
+    // t in one 16-B load (the plain order)
+    constexpr bool kH = XT::kBytes == 2;
+    f32x4 a[kH ? 1 : kLKS];
+    uint4 hb[kH ? kLKB : 1];
+    float rm = 0.f;  // max |x| of this lane's part of the row
+    if constexpr (kH) {
+      const uint16_t* xh = reinterpret_cast<const uint16_t*>(x) + (rin ? row : rows - 1) * ldx + 8 * g;
 #pragma unroll
-    for (int s = 0; s < kLKS; ++s) {
-      if (s >= KS) {
-        a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-        continue;
-      }
-      if (s < ksf) {
-        a[s] = load4<XT>(xr + 16 * s);
-      } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
+      for (int tt = 0; tt < kLKB; ++tt) {
+        const int f0 = 32 * tt + 8 * g;
+        if (tt < KB && f0 + 8 <= F) {
+          hb[tt] = *reinterpret_cast<const uint4*>(xh + 32 * tt);
+        } else {  // ragged tail: guarded scalar loads (never past the row)
+          uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) a[s][u] = 16 * s + 4 * g + u < F ? xcvt(xr[16 * s + u]) : 0.f;
-      } else {
-        a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int j = 0; j < 8; ++j)
+            if (tt < KB && f0 + j < F) w[j >> 1] |= uint32_t(xh[32 * tt + j]) << (16 * (j & 1));
+          hb[tt] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
       }
+#pragma unroll
+      for (int tt = 0; tt < kLKB; ++tt) {
+        const uint32_t w[4] = {hb[tt].x, hb[tt].y, hb[tt].z, hb[tt].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          rm = fmaxf(rm, fmaxf(fabsf(__uint_as_float(w[i] << 16)),
+                               fabsf(__uint_as_float(w[i] & 0xffff0000u))));
+      }
+    } else {
+      const typename XT::T* xr = x + (rin ? row : rows - 1) * ldx + 4 * g;
+#pragma unroll
+      for (int s = 0; s < kLKS; ++s) {
+        if (s >= KS) {
+          a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+        if (s < ksf) {
+          a[s] = load4<XT>(xr + 16 * s);
+        } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) a[s][u] = 16 * s + 4 * g + u < F ? xcvt(xr[16 * s + u]) : 0.f;
+        } else {
+          a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        rm = fmaxf(fmaxf(rm, fmaxf(fabsf(a[s].x), fabsf(a[s].y))), fmaxf(fabsf(a[s].z), fabsf(a[s].w)));
     }
     const bool lone = rin && rowptr[row + 1] - rowptr[row] == 1;
-    float rm = 0.f;  // max |x| of this lane's part of the row
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-      rm = fmaxf(fmaxf(rm, fmaxf(fabsf(a[s].x), fabsf(a[s].y))), fmaxf(fabsf(a[s].z), fabsf(a[s].w)));
     am = fmaxf(am, rm);  // clamped tail rows repeat row rows - 1: harmless for a max
     const bool any_lone = __ballot(lone) != 0;  // wave-uniform
     const int er = scale_exp(max_xor16_32(rm));  // lanes r, r + 16, r + 32, r + 48
@@ -108,8 +139,14 @@ k_logits_lone(
       union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const f32x4& src = a[2 * tt + (i >> 1)];
-        const f32x2 v = f32x2{src[2 * (i & 1)], src[2 * (i & 1) + 1]} * f32x2{rs, rs};
+        f32x2 v;
+        if constexpr (kH) {
+          const uint32_t w = i == 0 ? hb[tt].x : i == 1 ? hb[tt].y : i == 2 ? hb[tt].z : hb[tt].w;
+          v = f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)} * f32x2{rs, rs};
+        } else {
+          const f32x4& src = a[2 * tt + (i >> 1)];
+          v = f32x2{src[2 * (i & 1)], src[2 * (i & 1) + 1]} * f32x2{rs, rs};
+        }
         hi.p[i] = __builtin_convertvector(v, f16x2);
         lo.u[i] = split_lo(v, hi.u[i]);
       }
@@ -185,13 +222,14 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
   const int64_t cap = int64_t(cu_count()) * 2;  // resident blocks; grid-stride beyond
   if (nb > cap) nb = cap;
   auto kern = F <= 176 ? &k_logits_lone<XT, 11> : &k_logits_lone<XT, 12>;
+  const bool plain = XT::kBytes == 2;  // bf16: plain-order fragments (16-B loads)
   kern<<<int(nb), kLLWaves * 64, 0, stream>>>(
       static_cast<const typename XT::T*>(x), rows, F, ldx,
       reinterpret_cast<const PackHeader*>(packed + L.hdr_off),
-      reinterpret_cast<const uint4*>(packed + L.uph_off),
-      reinterpret_cast<const uint4*>(packed + L.upl_off),
-      reinterpret_cast<const uint4*>(packed + L.wph_off),
-      reinterpret_cast<const uint4*>(packed + L.wpl_off), rowptr, bias, slope, st, xmax, out,
+      reinterpret_cast<const uint4*>(packed + (plain ? L.ush_off : L.uph_off)),
+      reinterpret_cast<const uint4*>(packed + (plain ? L.usl_off : L.upl_off)),
+      reinterpret_cast<const uint4*>(packed + (plain ? L.wbh_off : L.wph_off)),
+      reinterpret_cast<const uint4*>(packed + (plain ? L.wbl_off : L.wpl_off)), rowptr, bias, slope, st, xmax, out,
       stats, ep);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
@@ -203,9 +241,10 @@ namespace gfd {
 namespace fwd {
 
 bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx) {
-  const int eb = xdt == GFD_DTYPE_BF16 ? 2 : 4;
+  // fp32: 16-B loads of 4 features; bf16: 16-B loads of 8
   const uintptr_t a = reinterpret_cast<uintptr_t>(x);
-  return F >= 1 && F <= 16 * kLKS && a % (4 * eb) == 0 && ldx % 4 == 0;
+  const int per = xdt == GFD_DTYPE_BF16 ? 8 : 4;
+  return F >= 1 && F <= 16 * kLKS && a % 16 == 0 && ldx % per == 0;
 }
 
 gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,

@@ -169,13 +169,16 @@ __global__ void k_pack_wbar_perm(const float* __restrict__ W, int F, int KB,
   wpl[idx] = lo.v;
 }
 
-// [U | V] fragments in the same lane order as k_pack_wbar_perm (one 16-column
-// tile: column n = q of uv, K = features), power-of-two scaled by max |uv| ->
-// [2^13, 2^14), f16 hi / lo.  One block: the max, then the fragments.
+// [U | V] fragments (one 16-column tile: column n = q of uv, K = features),
+// power-of-two scaled by max |uv| -> [2^13, 2^14), f16 hi / lo, in the lane
+// order of k_pack_wbar_perm (fp32 logits pass) and in the plain order of
+// k_pack_wbar (bf16 logits pass).  One block: the max, then the fragments.
 __global__ void __launch_bounds__(256) k_pack_uv_perm(const float* __restrict__ uv, int F, int Fu,
                                                       int KB, PackHeader* __restrict__ hdr,
                                                       uint4* __restrict__ uph,
-                                                      uint4* __restrict__ upl) {
+                                                      uint4* __restrict__ upl,
+                                                      uint4* __restrict__ ush,
+                                                      uint4* __restrict__ usl) {
   __shared__ float red[256];
   const int t = threadIdx.x;
   float m = 0.f;
@@ -192,20 +195,22 @@ __global__ void __launch_bounds__(256) k_pack_uv_perm(const float* __restrict__ 
     hdr->uv_scale = sc;
     hdr->uv_unscale = ldexpf(1.0f, -ku);
   }
-  for (int idx = t; idx < KB * 64; idx += 256) {  // (k-step, lane)
-    const int lane = idx & 63, kt = idx >> 6;
+  for (int idx = t; idx < 2 * KB * 64; idx += 256) {  // (order, k-step, lane)
+    const bool plain = idx >= KB * 64;
+    const int i = plain ? idx - KB * 64 : idx;
+    const int lane = i & 63, kt = i >> 6;
     const int n = lane & 15, g = lane >> 4;
     union { uint4 v; _Float16 h[8]; } hi, lo;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int f = 32 * kt + 4 * g + j + (j >= 4 ? 12 : 0);
+      const int f = plain ? 32 * kt + 8 * g + j : 32 * kt + 4 * g + j + (j >= 4 ? 12 : 0);
       const float v = f < F ? uv[n * Fu + f] * sc : 0.f;
       const _Float16 hv = (_Float16)v;
       hi.h[j] = hv;
       lo.h[j] = (_Float16)(v - (float)hv);
     }
-    uph[idx] = hi.v;
-    upl[idx] = lo.v;
+    (plain ? ush : uph)[i] = hi.v;
+    (plain ? usl : upl)[i] = lo.v;
   }
 }
 
@@ -400,7 +405,9 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   GFD_LAUNCH_CHECK();
   k_pack_uv_perm<<<1, 256, 0, stream>>>(reinterpret_cast<const float*>(p + L.uv_off), F, L.Fu,
                                         L.KB, hdr, reinterpret_cast<uint4*>(p + L.uph_off),
-                                        reinterpret_cast<uint4*>(p + L.upl_off));
+                                        reinterpret_cast<uint4*>(p + L.upl_off),
+                                        reinterpret_cast<uint4*>(p + L.ush_off),
+                                        reinterpret_cast<uint4*>(p + L.usl_off));
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
