@@ -57,6 +57,8 @@ def parse(argv=None):
     p.add_argument("--edges", type=int, default=None)
     p.add_argument("--features", type=int, default=166)
     p.add_argument("--gamma", type=float, default=2.1)
+    p.add_argument("--row-align", type=int, default=16,
+                   help="byte alignment of x rows (16: pitch 168; 128: whole cache lines)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-legs", action="store_true")
     p.add_argument("--legs", default="c4bwd,sample,c5,c1,c2,c3,temporal,ingest",
@@ -75,7 +77,8 @@ def glorot(shape, gen, device):
     return (torch.rand(shape, generator=gen) * 2 * a - a).to(device)
 
 
-def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, world=1):
+def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, world=1,
+          row_align=16):
     """The bench workload, built on the device exactly as timed: Chung-Lu
     graph (seed 1) -> CSR, x ~ N(0,1) (seed 0) at a 16-B row pitch, glorot W
     (seed 0), zero bias, this rank's destination shard and its cached plan.
@@ -87,7 +90,9 @@ def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, worl
     torch.cuda.empty_cache()
     gx = torch.Generator(device=dev).manual_seed(0)
     esz = torch.tensor([], dtype=dtype).element_size()
-    ldx = (F * esz + 15) // 16 * 16 // esz  # 16-B aligned rows: pitch 168 for F = 166
+    # rows aligned to row_align bytes: 16 -> pitch 168 for F = 166; 128 -> whole
+    # 128-B lines per row (pitch 192: fp32 6 lines, bf16 3 lines per gathered row)
+    ldx = (F * esz + row_align - 1) // row_align * row_align // esz
     xbuf = torch.randn((nodes, ldx), generator=gx, device=dev, dtype=torch.float32).to(dtype)
     x = xbuf[:, :F]
     gen = torch.Generator().manual_seed(0)
@@ -330,7 +335,7 @@ def measure(args, dev, rank, world, config):
     else:
         N, E, dtype = args.nodes or 10_000_000, args.edges or 50_000_000, torch.float32
     t_setup = time.perf_counter()
-    s = setup(dev, N, E, F, args.gamma, dtype, rank, world)
+    s = setup(dev, N, E, F, args.gamma, dtype, rank, world, row_align=args.row_align)
     layer = Layer(s, dev, world)
     plan = layer.plan
     esz = s["xbuf"].element_size()

@@ -160,10 +160,12 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF>& q, in
     // weights, so z comes out normalised and scaled and only needs the split
     const float ps = p * (inv * ldexpf(1.0f, erg));
     if (kmax <= 2) fma_k<KF, 2>(z, q.xv, ps);
+    else if (kmax == 3) fma_k<KF, 3>(z, q.xv, ps);
     else fma_k<KF, 4>(z, q.xv, ps);
     split_zrow<KF>(z, hi, lo);
   } else {
     if (kmax <= 2) fma_k<KF, 2>(z, q.xv, p);
+    else if (kmax == 3) fma_k<KF, 3>(z, q.xv, p);
     else fma_k<KF, 4>(z, q.xv, p);
     er = pack_zrow<KF>(z, inv, erg, hi, lo);
   }
