@@ -57,6 +57,15 @@ constexpr int kSWaves = 8;
 template <bool LIGHT>
 constexpr int ap_of() { return LIGHT ? GFD_LIGHT_AP : GFD_GENERAL_AP; }
 
+#ifdef GFD_PROF
+// Diagnostic build only (GFD_BUILD_VARIANT=prof GFD_EXTRA_FLAGS=-DGFD_PROF):
+// per-wave s_memtime cycles of the tile loop phases, summed over waves,
+// [light][phase]: 0 MFMA + next-tile issue, 1 barrier 1, 2 aggregation,
+// 3 barrier 2; [light][4] tiles; [light][5] cycles from the loop top to the
+// end of k-step 0 (the first issue piece: waits for the slot records).  Read by gfd_prof_read (scripts/prof_phases.py).
+__device__ unsigned long long g_prof[2][6];
+#endif
+
 struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm queue)
   int v;          // lanes 0..3: {row, e_begin, e_end, hub_rank}; lanes 8..15: sources of
                   // messages 0..7 (slot_cols); other lanes: row
@@ -416,7 +425,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     }
   };
   f32x4 acc_prev = {0.f, 0.f, 0.f, 0.f};  // kh = 0: tile v - 1, stored during MFMA(v)
+#ifdef GFD_PROF
+  unsigned long long pc[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
+#endif
   for (int64_t v = 0; v < nv; ++v) {
+#ifdef GFD_PROF
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
     lane = opaque(threadIdx.x & 63);
     const int par = int(v & 1);
     // ---- MFMA: out[16 x 16] of column tile ct over K half kh ----
@@ -465,6 +480,9 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       }
 #undef GFD_PIECE
       if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
+#ifdef GFD_PROF
+      if (u == 1) pc[4] += __builtin_amdgcn_s_memtime() - ts0;
+#endif
       if (u < KH) {
         const f16x8 ahi = phi[u % kAP], alo = plo[u % kAP];
         f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % kAP];
@@ -486,12 +504,36 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     acc0 += acc1;
     if (kh) red0[(par * 4 + ct) * 64 + lane] = acc0;
     acc_prev = acc0;
+#ifdef GFD_PROF
+    const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();  // partials visible; every Z read of this tile done
+#ifdef GFD_PROF
+    const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- tile v + 1: aggregate its rows into Z ----
     if (more) aggregate(pn);
+#ifdef GFD_PROF
+    const unsigned long long ts3 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();  // Z of the next tile complete
+#ifdef GFD_PROF
+    const unsigned long long ts4 = __builtin_amdgcn_s_memtime();
+    pc[0] += ts1 - ts0;
+    pc[1] += ts2 - ts1;
+    pc[2] += ts3 - ts2;
+    pc[3] += ts4 - ts3;
+#endif
   }
+#ifdef GFD_PROF
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_prof[LIGHT ? 1 : 0][i], pc[i]);
+    if (wave == 0) atomicAdd(&g_prof[LIGHT ? 1 : 0][4], (unsigned long long)nv);
+    atomicAdd(&g_prof[LIGHT ? 1 : 0][5], pc[4]);
+  }
+#endif
 #undef GFD_ISSUE
   if (!kh) reduce_store(acc_prev, int((nv - 1) & 1));  // last tile
 }
@@ -570,3 +612,14 @@ gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
 
 }  // namespace fwd
 }  // namespace gfd
+
+#ifdef GFD_PROF
+extern "C" int gfd_prof_read(unsigned long long* out12, int reset) {
+  if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_prof), sizeof(g_prof)) != hipSuccess) return 1;
+  if (reset) {
+    static const unsigned long long zero[2][6] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
