@@ -12,6 +12,15 @@ constexpr int kWave = 64;
 constexpr int kHeads = 8;      // the reference hard-codes heads=8 (gat.py:39,45,51)
 constexpr int kChannels = 64;  // hidden_channels=64 (config.py:32)
 constexpr float kSoftmaxEps = 1e-16f;  // PyG utils.softmax denominator epsilon
+// Messages (self loop included) of the largest "light" destination of the tile
+// stage: every row prefetched one tile ahead (gfd_stream.hip); the plan's class
+// split (k_slot_desc) uses the same bound.  6 measured against 4 and 5
+// (scripts/gpu_ab.sh, -DGFD_LIGHT_MAX=n variants): C5 105.0 -> 101.2 ms, C4
+// unchanged within noise.
+#ifndef GFD_LIGHT_MAX
+#define GFD_LIGHT_MAX 6
+#endif
+constexpr int kLightMax = GFD_LIGHT_MAX;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -6,8 +6,8 @@
 //   out_i = sum_h W_h z_ih / H + bias   (MFMA over K = 8 * Fp)
 // Destinations are scheduled by class (the plan's descending-degree slot order):
 //   hubs  (> threshold messages)   k_hub_partial / k_hub_fin   (gfd_hub.hip)
-//   general (hub rows, 5+ msgs)    k_stream<LIGHT = false>  8 waves, W stationary
-//   light (2..4 messages)          k_stream<LIGHT = true>   (gfd_stream.hip)
+//   general (hub rows, 7+ msgs)    k_stream<LIGHT = false>  8 waves, W stationary
+//   light (2..kLightMax = 6 msgs)  k_stream<LIGHT = true>   (gfd_stream.hip)
 //   lone  (self loop only)         k_lone   out = mean_h W_h x_i  (gfd_lone.hip)
 //   F > 168 / no plan              k_fused  (gfd_fused.hip)
 #pragma once
@@ -320,8 +320,9 @@ __device__ __forceinline__ void fma_rows(f32x2 (&z)[4][KF], const float (&xr)[NR
 
 // z = sum over the first K rows of p_k x_k (no per-message branches: rows past
 // the slot's messages carry p = 0 on valid prefetched rows)
-template <int KF, int K>
-__device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[4][KF], float pv) {
+template <int KF, int K, int NR>
+__device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[NR][KF], float pv) {
+  static_assert(K <= NR, "rows past the prefetched ones");
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll

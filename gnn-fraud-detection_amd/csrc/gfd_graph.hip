@@ -152,7 +152,7 @@ __global__ void k_order_keys(const int32_t* __restrict__ rowptr, int64_t n, int3
 // (clamped to the last one): one 16-B + one 32-B load replace the
 // order -> hub_rank -> rowptr -> col chain of dependent loads in the tile kernel.
 // Also the class boundaries of the tile stage (max over slots of 1 + the slot
-// index of every hub / > 4-message slot, and of every hub / > 1-message slot):
+// index of every hub / > kLightMax-message slot, and of every hub / > 1-message slot):
 // exact for any slot order.
 __global__ void k_slot_desc(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                             int64_t n, const int32_t* __restrict__ order,
@@ -169,7 +169,7 @@ __global__ void k_slot_desc(const int32_t* __restrict__ rowptr, const int32_t* _
 #pragma unroll
       for (int k = 0; k < 8; ++k) cols8[s * 8 + k] = col[min(b + k, e - 1)];
     }
-    if (hr >= 0 || e - b > 4) s_gen = (unsigned long long)(s + 1);
+    if (hr >= 0 || e - b > kLightMax) s_gen = (unsigned long long)(s + 1);
     if (hr >= 0 || e - b > 1) s_light = (unsigned long long)(s + 1);
   }
   if (split) {

@@ -12,9 +12,10 @@
 //  * Z goes through LDS once per 16-row tile in the feature-major K order
 //    p = 8 f + h, so a lane stores all 8 heads of its feature with one 16-B
 //    write per (hi, lo).  acc += Zhi.Whi + Zhi.Wlo + Zlo.Whi (lo unscaled).
-//  * Two destinations per wave (rows 2w, 2w+1).  The first 4 x rows of a slot
-//    (all of a light slot's) are issued one tile ahead, between the MFMA
-//    k-steps of the current tile; records are loaded two tiles ahead.
+//  * Two destinations per wave (rows 2w, 2w+1).  The first 4 x rows of a
+//    general slot (all kLightMax of a light slot's) are issued one tile
+//    ahead, between the MFMA k-steps of the current tile; records are loaded
+//    two tiles ahead.
 //  * General slots (LIGHT = false) continue with an online softmax over
 //    batches of 8 messages: the sources of messages 8..71 come with the
 //    record (one 64-wide window of the CSR columns), so the logits and all 8
@@ -77,12 +78,12 @@ struct SlotRing {  // a slot record parked in LDS between issue and aggregation
   int j[8];        // sources of messages 0..7 (general slots)
 };
 
-template <int KF>
+template <int KF, int NRW = 4>
 struct SlotRows {  // a slot's first (and, for light slots, only) batch in flight
   float th;        // t_i of head lane & 7
   float sj;        // s_j of the lane's message (lane >> 3)
   int cj;          // general: source of message 8 + lane (0 past the end)
-  float xv[4][KF];  // x rows of messages 0..3 (lane <-> feature)
+  float xv[NRW][KF];  // x rows of messages 0 .. NRW - 1 (lane <-> feature)
 };
 
 // live: slot < lim (<= num_dst): the light launch stops at the first lone slot
@@ -101,8 +102,8 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
 // window (general) and the ring record; part 1 + k = x row k.  Issued
 // unconditionally (past the last slot: clamped, ignored records), so no
 // branch joins in-flight loads.
-template <int PART, typename XT, int KF, bool LIGHT>
-__device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF>& q,
+template <int PART, typename XT, int KF, bool LIGHT, int NRW>
+__device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW>& q,
                                               const void* __restrict__ x, int64_t ldx, int F,
                                               const int32_t* __restrict__ col,
                                               const float* __restrict__ st, int64_t dst_offset,
@@ -136,11 +137,24 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF>& q,
   }
 }
 
-// A slot with at most 4 messages (all rows prefetched), not a hub, no dropout:
-// straight-line code, the softmax sum and reciprocal independent of the FMA
-// block.  kmax: messages to run (wave-uniform, >= n).
+// z = sum of the first kmax (2 .. kLightMax, wave-uniform) rows, one
+// straight-line block per count
 template <int KF>
-__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF>& q, int kmax,
+__device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[kLightMax][KF],
+                                          float p, int kmax) {
+  static_assert(kLightMax >= 4 && kLightMax <= 6, "light slots: 4 .. 6 messages");
+  if (kmax <= 2) fma_k<KF, 2>(z, xv, p);
+  else if (kmax == 3) fma_k<KF, 3>(z, xv, p);
+  else if (kLightMax == 4 || kmax == 4) fma_k<KF, 4>(z, xv, p);
+  else if (kLightMax == 5 || kmax == 5) fma_k<KF, (kLightMax >= 5 ? 5 : 4)>(z, xv, p);
+  else fma_k<KF, kLightMax>(z, xv, p);
+}
+
+// A slot with at most kLightMax messages (all rows prefetched), not a hub, no
+// dropout: straight-line code, the softmax sum and reciprocal independent of
+// the FMA block.  kmax: messages to run (wave-uniform, >= n).
+template <int KF>
+__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLightMax>& q, int kmax,
                                          float slope, int Fp, float* __restrict__ stats,
                                          _Float16* __restrict__ zh, _Float16* __restrict__ zl,
                                          float* __restrict__ rsc, int* __restrict__ rid, int r,
@@ -168,14 +182,10 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF>& q, in
     // one scale for every row: fold 1 / (sum + eps) and 2^erg into the
     // weights, so z comes out normalised and scaled and only needs the split
     const float ps = p * (inv * ldexpf(1.0f, erg));
-    if (kmax <= 2) fma_k<KF, 2>(z, q.xv, ps);
-    else if (kmax == 3) fma_k<KF, 3>(z, q.xv, ps);
-    else fma_k<KF, 4>(z, q.xv, ps);
+    light_fma<KF>(z, q.xv, ps, kmax);
     split_zrow<KF>(z, hi, lo);
   } else {
-    if (kmax <= 2) fma_k<KF, 2>(z, q.xv, p);
-    else if (kmax == 3) fma_k<KF, 3>(z, q.xv, p);
-    else fma_k<KF, 4>(z, q.xv, p);
+    light_fma<KF>(z, q.xv, p, kmax);
     er = pack_zrow<KF>(z, inv, erg, hi, lo);
   }
   write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
@@ -375,7 +385,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   if (nv == 0) return;  // uniform per block: no barrier below is reached by anyone
 
   SlotRec n0, n1;
-  SlotRows<KF> d0, d1;
+  constexpr int NL = LIGHT ? kLightMax : 4;  // rows issued one tile ahead per slot
+  SlotRows<KF, NL> d0, d1;
   // prologue: tile 0 issued and aggregated; records of tile 1 loading
   sl_rec(n0, slot(0, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(0, r1), num_dst, lim, desc, cols8, lane);
@@ -384,9 +395,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   GFD_ISSUE(0, n0, d0, ring0 + r0); GFD_ISSUE(1, n0, d0, ring0 + r0);
   GFD_ISSUE(2, n0, d0, ring0 + r0); GFD_ISSUE(3, n0, d0, ring0 + r0);
   GFD_ISSUE(4, n0, d0, ring0 + r0);
+  if constexpr (NL >= 5) GFD_ISSUE((NL >= 5 ? 5 : 4), n0, d0, ring0 + r0);
+  if constexpr (NL >= 6) GFD_ISSUE((NL >= 6 ? 6 : 4), n0, d0, ring0 + r0);
   GFD_ISSUE(0, n1, d1, ring0 + r1); GFD_ISSUE(1, n1, d1, ring0 + r1);
   GFD_ISSUE(2, n1, d1, ring0 + r1); GFD_ISSUE(3, n1, d1, ring0 + r1);
   GFD_ISSUE(4, n1, d1, ring0 + r1);
+  if constexpr (NL >= 5) GFD_ISSUE((NL >= 5 ? 5 : 4), n1, d1, ring0 + r1);
+  if constexpr (NL >= 6) GFD_ISSUE((NL >= 6 ? 6 : 4), n1, d1, ring0 + r1);
   sl_rec(n0, slot(1, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, lim, desc, cols8, lane);
   auto aggregate = [&](int tpar) {  // this wave's two slots of the tile in parity tpar
@@ -458,26 +473,26 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #pragma unroll
     for (int u = 0; u < KHM; ++u) {
       // the next tile's rows are issued between the k-steps (the vector memory
-      // pipe is idle in this phase): 10 pieces (per slot: header, 4 rows)
-      // spread evenly, piece i in k-step i * KHM / 10
+      // pipe is idle in this phase): 2 NL + 2 pieces (per slot: header, NL
+      // rows) spread evenly, piece i in k-step i * KHM / (2 NL + 2)
       SlotRing* rg = ring0 + pn * kTile;
-#define GFD_PIECE(i) (u == (i) * KHM / 10)
+#define GFD_PIECE(i) (u == (i) * KHM / (2 * NL + 2))
       if (GFD_PIECE(0)) GFD_ISSUE(0, n0, d0, rg + r0);
       if (GFD_PIECE(1)) GFD_ISSUE(1, n0, d0, rg + r0);
       if (GFD_PIECE(2)) GFD_ISSUE(2, n0, d0, rg + r0);
       if (GFD_PIECE(3)) GFD_ISSUE(3, n0, d0, rg + r0);
-      if (GFD_PIECE(4)) {
-        GFD_ISSUE(4, n0, d0, rg + r0);
-        sl_rec(n0, slot(v + 2, r0), num_dst, lim, desc, cols8, lane);
-      }
-      if (GFD_PIECE(5)) GFD_ISSUE(0, n1, d1, rg + r1);
-      if (GFD_PIECE(6)) GFD_ISSUE(1, n1, d1, rg + r1);
-      if (GFD_PIECE(7)) GFD_ISSUE(2, n1, d1, rg + r1);
-      if (GFD_PIECE(8)) GFD_ISSUE(3, n1, d1, rg + r1);
-      if (GFD_PIECE(9)) {
-        GFD_ISSUE(4, n1, d1, rg + r1);
-        sl_rec(n1, slot(v + 2, r1), num_dst, lim, desc, cols8, lane);
-      }
+      if (GFD_PIECE(4)) GFD_ISSUE(4, n0, d0, rg + r0);
+      if constexpr (NL >= 5) if (GFD_PIECE(5)) GFD_ISSUE((NL >= 5 ? 5 : 4), n0, d0, rg + r0);
+      if constexpr (NL >= 6) if (GFD_PIECE(6)) GFD_ISSUE((NL >= 6 ? 6 : 4), n0, d0, rg + r0);
+      if (GFD_PIECE(NL)) sl_rec(n0, slot(v + 2, r0), num_dst, lim, desc, cols8, lane);
+      if (GFD_PIECE(NL + 1)) GFD_ISSUE(0, n1, d1, rg + r1);
+      if (GFD_PIECE(NL + 2)) GFD_ISSUE(1, n1, d1, rg + r1);
+      if (GFD_PIECE(NL + 3)) GFD_ISSUE(2, n1, d1, rg + r1);
+      if (GFD_PIECE(NL + 4)) GFD_ISSUE(3, n1, d1, rg + r1);
+      if (GFD_PIECE(NL + 5)) GFD_ISSUE(4, n1, d1, rg + r1);
+      if constexpr (NL >= 5) if (GFD_PIECE(NL + 6)) GFD_ISSUE((NL >= 5 ? 5 : 4), n1, d1, rg + r1);
+      if constexpr (NL >= 6) if (GFD_PIECE(NL + 7)) GFD_ISSUE((NL >= 6 ? 6 : 4), n1, d1, rg + r1);
+      if (GFD_PIECE(2 * NL + 1)) sl_rec(n1, slot(v + 2, r1), num_dst, lim, desc, cols8, lane);
 #undef GFD_PIECE
       if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
 #ifdef GFD_PROF

@@ -136,9 +136,9 @@ gfd_status gfd_plan_order(const int32_t* rowptr, int64_t num_dst, int32_t cap, i
  * + k, e_end - 1)] (the first 8 sources, prefetched one tile ahead).
  * class_split (nullable, device int64[2]) receives the slot class boundaries
  * the forward's tile stage schedules by: class_split[0] = 1 + the last slot
- * that is a hub or has more than 4 messages, class_split[1] = 1 + the last
+ * that is a hub or has more than 6 messages, class_split[1] = 1 + the last
  * slot that is a hub or has more than 1 message (0 when there is none).
- * Slots past class_split[0] are "light" (2..4 messages), slots past
+ * Slots past class_split[0] are "light" (2..6 messages), slots past
  * class_split[1] "lone" (self loop only).  Correct for ANY order: an order
  * that is not degree-sorted only moves the boundaries towards num_dst. */
 gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t num_dst,
