@@ -362,7 +362,7 @@ def measure(args, dev, rank, world, config):
     kname = {"pack+logits": "k_logits_s (+ pack)",
              "pack+logits+lone": "k_logits_lone (+ pack): logits + self-loop-only rows",
              "hubs": "k_hub_partial + k_hub_fin",
-             "general": "k_stream<general> (hub rows, 5+ messages)",
+             "general": "k_stream<general> (hub rows, 7+ messages)",
              "light": "k_stream<light> (2-6 messages)",
              "lone": "k_lone (self-loop-only rows)"}
     pmc = load_pmc(args.pmc, f"{config}:{dom}:N={N}:E={E}:F={F}:world={world}")
