@@ -49,14 +49,21 @@ namespace {
 
 constexpr int kSWaves = 8;
 #ifndef GFD_LIGHT_AP
-#define GFD_LIGHT_AP 2
+#define GFD_LIGHT_AP 1
+#endif
+#ifndef GFD_LIGHT_AP_BF16
+#define GFD_LIGHT_AP_BF16 2
 #endif
 #ifndef GFD_GENERAL_AP
 #define GFD_GENERAL_AP 1
 #endif
-// A-fragment k-steps read ahead in the MFMA loop (general, light)
-template <bool LIGHT>
-constexpr int ap_of() { return LIGHT ? GFD_LIGHT_AP : GFD_GENERAL_AP; }
+// A-fragment k-steps read ahead in the MFMA loop (general; light fp32 / bf16
+// rows).  Light fp32: 1 keeps the kernel spill-free with 6 rows per slot in
+// flight (C4 light 6.73 -> 6.22 ms against 2); light bf16: 2 (C5 33.3 vs 33.7 ms)
+template <bool LIGHT, typename XT>
+constexpr int ap_of() {
+  return LIGHT ? (XT::kBytes == 2 ? GFD_LIGHT_AP_BF16 : GFD_LIGHT_AP) : GFD_GENERAL_AP;
+}
 
 #ifdef GFD_PROF
 // Diagnostic build only (GFD_BUILD_VARIANT=prof GFD_EXTRA_FLAGS=-DGFD_PROF):
@@ -457,7 +464,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     // A fragments (and LDS-resident W_lo) kAP k-steps ahead; the scheduling
     // barriers keep the compiler from hoisting every LDS read of the tile
     // (registers belong to W)
-    constexpr int kAP = ap_of<LIGHT>();
+    constexpr int kAP = ap_of<LIGHT, XT>();
     f16x8 phi[kAP], plo[kAP], pwl[kAP];
 #pragma unroll
     for (int u = 0; u < kAP; ++u) {
