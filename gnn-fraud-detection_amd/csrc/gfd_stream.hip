@@ -149,11 +149,12 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW
 template <int KF>
 __device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[kLightMax][KF],
                                           float p, int kmax) {
-  static_assert(kLightMax >= 4 && kLightMax <= 6, "light slots: 4 .. 6 messages");
+  static_assert(kLightMax >= 4 && kLightMax <= 7, "light slots: 4 .. 7 messages");
   if (kmax <= 2) fma_k<KF, 2>(z, xv, p);
   else if (kmax == 3) fma_k<KF, 3>(z, xv, p);
   else if (kLightMax == 4 || kmax == 4) fma_k<KF, 4>(z, xv, p);
   else if (kLightMax == 5 || kmax == 5) fma_k<KF, (kLightMax >= 5 ? 5 : 4)>(z, xv, p);
+  else if (kLightMax == 6 || kmax == 6) fma_k<KF, (kLightMax >= 6 ? 6 : 4)>(z, xv, p);
   else fma_k<KF, kLightMax>(z, xv, p);
 }
 
@@ -404,11 +405,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   GFD_ISSUE(4, n0, d0, ring0 + r0);
   if constexpr (NL >= 5) GFD_ISSUE((NL >= 5 ? 5 : 4), n0, d0, ring0 + r0);
   if constexpr (NL >= 6) GFD_ISSUE((NL >= 6 ? 6 : 4), n0, d0, ring0 + r0);
+  if constexpr (NL >= 7) GFD_ISSUE((NL >= 7 ? 7 : 4), n0, d0, ring0 + r0);
   GFD_ISSUE(0, n1, d1, ring0 + r1); GFD_ISSUE(1, n1, d1, ring0 + r1);
   GFD_ISSUE(2, n1, d1, ring0 + r1); GFD_ISSUE(3, n1, d1, ring0 + r1);
   GFD_ISSUE(4, n1, d1, ring0 + r1);
   if constexpr (NL >= 5) GFD_ISSUE((NL >= 5 ? 5 : 4), n1, d1, ring0 + r1);
   if constexpr (NL >= 6) GFD_ISSUE((NL >= 6 ? 6 : 4), n1, d1, ring0 + r1);
+  if constexpr (NL >= 7) GFD_ISSUE((NL >= 7 ? 7 : 4), n1, d1, ring0 + r1);
   sl_rec(n0, slot(1, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, lim, desc, cols8, lane);
   auto aggregate = [&](int tpar) {  // this wave's two slots of the tile in parity tpar
@@ -491,6 +494,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       if (GFD_PIECE(4)) GFD_ISSUE(4, n0, d0, rg + r0);
       if constexpr (NL >= 5) if (GFD_PIECE(5)) GFD_ISSUE((NL >= 5 ? 5 : 4), n0, d0, rg + r0);
       if constexpr (NL >= 6) if (GFD_PIECE(6)) GFD_ISSUE((NL >= 6 ? 6 : 4), n0, d0, rg + r0);
+      if constexpr (NL >= 7) if (GFD_PIECE(7)) GFD_ISSUE((NL >= 7 ? 7 : 4), n0, d0, rg + r0);
       if (GFD_PIECE(NL)) sl_rec(n0, slot(v + 2, r0), num_dst, lim, desc, cols8, lane);
       if (GFD_PIECE(NL + 1)) GFD_ISSUE(0, n1, d1, rg + r1);
       if (GFD_PIECE(NL + 2)) GFD_ISSUE(1, n1, d1, rg + r1);
@@ -499,6 +503,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       if (GFD_PIECE(NL + 5)) GFD_ISSUE(4, n1, d1, rg + r1);
       if constexpr (NL >= 5) if (GFD_PIECE(NL + 6)) GFD_ISSUE((NL >= 5 ? 5 : 4), n1, d1, rg + r1);
       if constexpr (NL >= 6) if (GFD_PIECE(NL + 7)) GFD_ISSUE((NL >= 6 ? 6 : 4), n1, d1, rg + r1);
+      if constexpr (NL >= 7) if (GFD_PIECE(NL + 8)) GFD_ISSUE((NL >= 7 ? 7 : 4), n1, d1, rg + r1);
       if (GFD_PIECE(2 * NL + 1)) sl_rec(n1, slot(v + 2, r1), num_dst, lim, desc, cols8, lane);
 #undef GFD_PIECE
       if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
