@@ -1,6 +1,6 @@
 // gfd_fused.hip -- general-purpose fused tile kernel (PyG GATConv.forward,
 // concat=False; /root/reference/src/models/gat.py:80): used for F > 168 (four
-// feature chunks, outside k_stream / k_mid's register budget) and for plans
+// feature chunks, outside k_stream's register budget) and for plans
 // without slot descriptors.  16 destinations per block, one per wave.
 //   phase A  online softmax over the destination's CSR segment, x rows
 //            gathered once for all 8 heads (lane <-> feature), z in registers

@@ -51,7 +51,7 @@ inline PackLayout pack_layout(int F) {
   // head-major fragments (k_fused): K position p = h * Fp + f, lo scaled by 2^11
   L.whi_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
   L.wlo_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
-  // feature-major fragments (k_stream, k_mid): K position p = 8 f + h, lo unscaled
+  // feature-major fragments (k_stream): K position p = 8 f + h, lo unscaled
   L.wsh_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
   L.wsl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KS) * 4 * 64, 256);
   // head-mean matrix Wbar = mean_h W_h (k_lone): K position p = f, lo unscaled

@@ -85,7 +85,7 @@ __global__ void k_pack_frag(const float* __restrict__ W, int F, int Fp, int KS,
   wlo[idx] = lo.v;
 }
 
-// Feature-major fragments (k_stream, k_mid): K position p = 8 f + h (one 16-B Z
+// Feature-major fragments (k_stream): K position p = 8 f + h (one 16-B Z
 // store per feature holds all 8 heads), lo = v - hi unscaled (|lo| <= 2^3 for
 // the 2^14-scaled W; fp16 subnormals there cost < 2^-38 of the largest weight).
 __global__ void k_pack_frag_s(const float* __restrict__ W, int F, int KS,

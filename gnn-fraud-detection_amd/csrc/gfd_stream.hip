@@ -1,5 +1,5 @@
-// gfd_stream.hip -- general (hub rows and 5+ messages) and light (2..4
-// messages incl. the self loop) destinations: the PyG GATConv.forward
+// gfd_stream.hip -- general (hub rows and 7+ messages) and light (2..kLightMax
+// = 6 messages incl. the self loop) destinations: the PyG GATConv.forward
 // softmax-aggregate-project of /root/reference/src/models/gat.py:80 for the
 // bulk of a power-law graph.  One kernel template, two instances (LIGHT).
 //

@@ -212,17 +212,17 @@ def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torc
     """Destination-sharded GATConv forward (eval) on this rank's GPU.
 
     ``x`` is halo-resident (all N rows on every rank, row stride may be
-    padded), ``graph`` the full CSR.  Steps: pack weights -> logits of the
-    rank's node block -> RCCL all-gather of the ``[N, 16]`` logits -> fused
-    aggregate-project over the rank's destinations -> (optionally)
-    all-gather-v of the ``[n_dst, 64]`` outputs.
+    padded), ``graph`` the full CSR.  Steps: pack weights -> ``exchange_logits``
+    (one RCCL all-gather of the SOURCE logits ``[N, 8]``; t recomputed for the
+    rank's own destinations) and max|x| reduced -> fused aggregate-project over
+    the rank's destinations -> (optionally) all-gather-v of the ``[n_dst, 64]``
+    outputs.
     """
     if x.stride(1) != 1:
         raise ValueError("x rows must be contiguous")
     packed = pack_weights(weight, att_src, att_dst)
     xmax = torch.zeros(1, dtype=torch.float32, device=x.device)
-    st_local = shard_logits(x, packed, spec, xmax)
-    st = all_gather_rows(st_local, x.size(0), spec.world, group=group)
+    st = exchange_logits(x, packed, spec, xmax, group=group)
     if spec.world > 1:
         import torch.distributed as dist
         dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
@@ -268,19 +268,23 @@ def shard_aggregate_ep(h: torch.Tensor, graph, st: torch.Tensor, packed: torch.T
 
 
 def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, residual: bool,
-                          group=None) -> torch.Tensor:
+                          group=None, st: Optional[torch.Tensor] = None,
+                          xmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One layer body on this rank: source logits exchanged
     (``exchange_logits``) and max|x| reduced, the rank's destinations
     aggregated with BN / ReLU / residual in the store.  ``h`` is the layer
-    input for ALL N nodes (layer 0: the halo-resident features)."""
+    input for ALL N nodes (layer 0: the halo-resident features).  ``st`` /
+    ``xmax``: the logits table and max |h| when the caller already has them
+    (hidden layers: they arrive with the all-gathered rows)."""
     import torch.distributed as dist
     from .fused import bn_affine
     packed = pack_weights(conv.lin_src.weight.detach(), conv.att_src.detach(),
                           conv.att_dst.detach())
-    xmax = torch.zeros(1, dtype=torch.float32, device=h.device)
-    st = exchange_logits(h, packed, spec, xmax, group=group)
-    if spec.world > 1:
-        dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
+    if st is None:
+        xmax = torch.zeros(1, dtype=torch.float32, device=h.device)
+        st = exchange_logits(h, packed, spec, xmax, group=group)
+        if spec.world > 1:
+            dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
     res = None
     if residual:
         res = h[spec.dst_lo:spec.dst_hi]
@@ -290,28 +294,71 @@ def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, res
                               bn_affine(bn, h.device), True, res)
 
 
+def gather_hidden(out_local: torch.Tensor, next_conv, spec: ShardSpec, group=None):
+    """The exchange before a hidden layer, as ONE collective: every rank
+    computes the next layer's logits [s | t] of its own output rows (they are
+    local), then all-gathers ``[out | s | max|out|]`` rows (all-gather-v,
+    72 columns).  Returns (h [N, 64] view with row stride 72, the [N, 16]
+    logits table -- s for every node, t for this rank's destinations -- and
+    max |h| over all rows, reduced over ranks by the same collective)."""
+    H, C = 8, 64
+    n_dst = out_local.size(0)
+    dev = out_local.device
+    packed = pack_weights(next_conv.lin_src.weight.detach(), next_conv.att_src.detach(),
+                          next_conv.att_dst.detach())
+    xmax_l = torch.zeros(1, dtype=torch.float32, device=dev)
+    st_l = logits_rows(out_local, packed, 0, n_dst, xmax_l)
+    rows = torch.empty((n_dst, C + H), dtype=torch.float32, device=dev)
+    rows[:, :C] = out_local
+    rows[:, C:] = st_l[:, :H]
+    # max |h| travels in an extra column of each rank's first row block: the
+    # padded row 0 of every block (all_gather_v pads to the largest block)
+    world = spec.world
+    sizes = [spec.dst_bounds[r + 1] - spec.dst_bounds[r] for r in range(world)]
+    per = max(max(sizes), 1) + 1
+    import torch.distributed as dist
+    buf = rows.new_zeros((per, C + H))
+    buf[0, 0] = xmax_l[0]
+    if n_dst:
+        buf[1:1 + n_dst] = rows
+    allb = rows.new_empty((per * world, C + H))
+    dist.all_gather_into_tensor(allb, buf, group=group)
+    xmax = allb[0::per, 0].max().reshape(1).contiguous()
+    full = torch.cat([allb[r * per + 1:r * per + 1 + sizes[r]] for r in range(world)])
+    st = torch.empty((full.size(0), 2 * H), dtype=torch.float32, device=dev)
+    st[:, :H] = full[:, C:]
+    if n_dst:
+        st[spec.dst_lo:spec.dst_hi, H:] = st_l[:, H:]
+    return full[:, :C], st, xmax
+
+
 def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=None,
                           gather_output: bool = True):
     """Destination-sharded eval forward of gfd.models.GAT / TemporalGNN (the
     reference's 2-3 layer stacks, gat.py:60-96, tgn.py:67-113) on this rank.
 
     Layer 0 reads the halo-resident features (all N rows on every rank; the
-    exchange is the [N, 16] logits all-gather).  Layers >= 1 need the previous
-    layer's output for every source: one all-gather-v of the [n_dst, 64]
-    shards (2.56 GB in total at C4, one RCCL collective over xGMI).  The heads
-    (Linear, GRUCell + Linear) are row-local.  Returns the outputs of the
-    rank's destinations, or of all N nodes (gather_output).  Inference only."""
+    exchange is the [N, 8] source-logits all-gather).  Before each layer >= 1
+    ONE collective (``gather_hidden``) moves the previous layer's output rows
+    together with the next layer's source logits, computed by the row's owner
+    (72 columns: 2.9 GB in total at C4) -- the logits exchange rides along
+    instead of costing a second collective.  The heads (Linear, GRUCell +
+    Linear) are row-local.  Returns the outputs of the rank's destinations, or
+    of all N nodes (gather_output).  Inference only."""
     if model.training or torch.is_grad_enabled():
         raise RuntimeError("model_forward_sharded is inference-only: model.eval() and no_grad")
     h = x
     L = len(model.gat_layers)
+    st = xmax = None
     for layer, conv in enumerate(model.gat_layers):
         bn = model.batch_norms[layer] if model.batch_norms is not None else None
         res = model.residual and h.size(-1) == model.hidden_channels
-        out_local = layer_forward_sharded(conv, bn, h, graph, spec, res, group)
+        out_local = layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax)
         if layer < L - 1:
-            h = (all_gather_v_rows(out_local, spec.dst_bounds, group=group)
-                 if spec.world > 1 else out_local)
+            if spec.world > 1:
+                h, st, xmax = gather_hidden(out_local, model.gat_layers[layer + 1], spec, group)
+            else:
+                h, st, xmax = out_local, None, None
         else:
             h = out_local
     if hasattr(model, "gru"):

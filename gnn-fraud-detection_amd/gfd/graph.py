@@ -253,31 +253,64 @@ def fingerprint(edge_index: torch.Tensor) -> Tuple[int, int]:
 _LOCK = threading.Lock()
 _BY_ID: dict = {}                      # id(edge_index) -> (weakref, key, graph)
 _BY_FP: "OrderedDict" = OrderedDict()  # (device, N, shape, fingerprint) -> graph
-_FP_CAP = 8
+_FP_CAP = 8                            # graphs held by content ...
+_FP_CAP_BYTES = 4 << 30                # ... and at most this many CSR bytes (LRU)
+# Edge lists that skip the content cache: per-batch subgraphs of the sampler
+# (gfd.sampler.NeighborLoader marks them) are used once, and would otherwise
+# flood the cache and pay a fingerprint sync each.
+_NO_FP: dict = {}                      # id(edge_index) -> weakref
+
+
+def no_content_cache(edge_index: torch.Tensor) -> torch.Tensor:
+    """Mark an edge list as single-use: ``get_graph`` builds its CSR without
+    fingerprinting it or keeping it in the content cache."""
+    oid = id(edge_index)
+    with _LOCK:
+        _NO_FP[oid] = weakref.ref(edge_index, lambda _r, oid=oid: _NO_FP.pop(oid, None))
+    return edge_index
+
+
+def _single_use(edge_index: torch.Tensor) -> bool:
+    with _LOCK:
+        r = _NO_FP.get(id(edge_index))
+    return r is not None and r() is edge_index
+
+
+def _graph_bytes(g: "CSRGraph") -> int:
+    return g.rowptr.numel() * 4 + g.col.numel() * 4
 
 
 def get_graph(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
     """Cached ``csr_from_coo``.  Fast path: the same tensor object (held
     weakly; its in-place version counter, storage pointer, shape and N are
-    part of the key).  Otherwise the content fingerprint: an equal edge list
-    in a new tensor reuses the CSR (and its plan / CSC) built for the first."""
+    part of the key).  Otherwise the content fingerprint: an equal edge list in a new tensor reuses
+    the CSR (and its plan / CSC) built for the first (edge lists marked by
+    ``no_content_cache`` skip this).  The content cache holds
+    at most ``_FP_CAP`` graphs and ``_FP_CAP_BYTES`` of CSR (least recently
+    used evicted first; ``clear_cache()`` drops everything)."""
     key = (edge_index._version, int(num_nodes), edge_index.data_ptr(), tuple(edge_index.shape))
     with _LOCK:
         ent = _BY_ID.get(id(edge_index))
         if ent is not None and ent[0]() is edge_index and ent[1] == key:
             return ent[2]
-    fkey = (str(edge_index.device), int(num_nodes), tuple(edge_index.shape),
-            fingerprint(edge_index))
-    with _LOCK:
-        g = _BY_FP.get(fkey)
-        if g is not None:
-            _BY_FP.move_to_end(fkey)
+    g = None
+    fkey = None
+    if not _single_use(edge_index):
+        fkey = (str(edge_index.device), int(num_nodes), tuple(edge_index.shape),
+                fingerprint(edge_index))
+        with _LOCK:
+            g = _BY_FP.get(fkey)
+            if g is not None:
+                _BY_FP.move_to_end(fkey)
     if g is None:
         g = csr_from_coo(edge_index, num_nodes)
-        with _LOCK:
-            _BY_FP[fkey] = g
-            while len(_BY_FP) > _FP_CAP:
-                _BY_FP.popitem(last=False)
+        if fkey is not None:
+            with _LOCK:
+                _BY_FP[fkey] = g
+                while len(_BY_FP) > 1 and (
+                        len(_BY_FP) > _FP_CAP or
+                        sum(_graph_bytes(v) for v in _BY_FP.values()) > _FP_CAP_BYTES):
+                    _BY_FP.popitem(last=False)
     oid = id(edge_index)
     ref = weakref.ref(edge_index, lambda _r, oid=oid: _BY_ID.pop(oid, None))
     with _LOCK:

@@ -58,16 +58,21 @@ def _upload(a: np.ndarray, device, chunk_bytes: int = 64 << 20) -> torch.Tensor:
     per = max(1, chunk_bytes // a.itemsize)
     bufs = [torch.empty(per, dtype=out.dtype).pin_memory() for _ in range(2)]
     events = [None, None]
-    for k, s in enumerate(range(0, flat_src.size, per)):
-        n = min(per, flat_src.size - s)
-        b = k & 1
-        if events[b] is not None:
-            events[b].synchronize()              # the copy out of this buffer is done
-        bufs[b][:n].numpy()[...] = flat_src[s:s + n]
-        flat_dst[s:s + n].copy_(bufs[b][:n], non_blocking=True)
-        events[b] = torch.cuda.Event()
-        events[b].record()
-    torch.cuda.current_stream(device).synchronize()
+    # the copies run on the destination device's current stream; every event
+    # is recorded there too (not on the current device's), so a pinned buffer
+    # is refilled only after the DMA out of it has finished
+    with torch.cuda.device(out.device):
+        stream = torch.cuda.current_stream(out.device)
+        for k, s in enumerate(range(0, flat_src.size, per)):
+            n = min(per, flat_src.size - s)
+            b = k & 1
+            if events[b] is not None:
+                events[b].synchronize()          # the copy out of this buffer is done
+            bufs[b][:n].numpy()[...] = flat_src[s:s + n]
+            flat_dst[s:s + n].copy_(bufs[b][:n], non_blocking=True)
+            events[b] = torch.cuda.Event()
+            events[b].record(stream)
+        stream.synchronize()
     return out
 
 

@@ -29,7 +29,25 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib
-from .graph import CSRGraph, _ws, get_graph
+from .graph import CSRGraph, _ws, get_graph, no_content_cache
+
+_M64 = 2 ** 64 - 1
+
+
+def _splitmix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def batch_seed(seed: int, epoch: int, batch: int) -> int:
+    """Per-batch sampling seed: the (seed, epoch, batch) tuple hashed field by
+    field (splitmix64 chained), so no two tuples share a draw stream the way
+    overlapping bit fields would (batch 2^20 of epoch e vs batch 0 of e + 1)."""
+    h = _splitmix64(int(seed) & _M64)
+    h = _splitmix64(h ^ (int(epoch) & _M64))
+    return _splitmix64(h ^ (int(batch) & _M64))
 
 
 @dataclass
@@ -76,6 +94,10 @@ class NeighborSampler:
         ns = seeds.numel()
         if ns == 0:
             raise ValueError("empty seed batch")
+        if torch.unique(seeds).numel() != ns:
+            # the relabelling keeps one local id per node: a repeated seed
+            # would silently lose its copy
+            raise ValueError("seed batch holds duplicate node ids")
         mn, me, ws = self._bounds(ns)
         n_id = torch.empty(mn, dtype=torch.int64, device=dev)
         level_ptr = torch.empty(self.hops + 2, dtype=torch.int64, device=dev)
@@ -95,7 +117,8 @@ class NeighborSampler:
             raise _lib.GfdError("gfd_sample_neighbors", st)
         lp, ep = level_ptr.tolist(), edge_ptr.tolist()
         n, e = lp[-1], ep[-1]
-        return SampledBatch(n_id[:n], torch.stack([esrc[:e], edst[:e]]), eid[:e], ns, lp, ep)
+        ei = no_content_cache(torch.stack([esrc[:e], edst[:e]]))   # single-use subgraph
+        return SampledBatch(n_id[:n], ei, eid[:e], ns, lp, ep)
 
 
 class NeighborLoader:
@@ -117,6 +140,8 @@ class NeighborLoader:
             idx = input_nodes.to(dev).nonzero().view(-1)
         else:
             idx = input_nodes.to(dev).long()
+            if torch.unique(idx).numel() != idx.numel():
+                raise ValueError("input_nodes holds duplicate node ids")
         self.input_nodes, self.batch_size, self.shuffle = idx, int(batch_size), shuffle
         self.seed, self.epoch = int(seed), 0
 
@@ -131,7 +156,7 @@ class NeighborLoader:
             idx = idx[torch.randperm(idx.numel(), generator=gen, device=idx.device)]
         for b in range(len(self)):
             seeds = idx[b * self.batch_size:(b + 1) * self.batch_size]
-            batch = self.sampler.sample(seeds, seed=(self.seed << 32) ^ (self.epoch << 20) ^ b)
+            batch = self.sampler.sample(seeds, seed=batch_seed(self.seed, self.epoch, b))
             batch.x = self.x[batch.n_id]
             if self.y is not None:
                 batch.y = self.y[batch.n_id]

@@ -21,7 +21,8 @@
  *    (GFD_DTYPE_BF16, config C5), row-major with any row pitch; every other
  *    floating-point argument is IEEE fp32.  Internally the feature projection
  *    runs on f16 MFMA with a 3-term hi/lo split over power-of-two scaled rows
- *    (~2^-21 relative, fp32-faithful); logits are exact fp32 MFMA; softmax,
+ *    (~2^-21 relative, fp32-faithful); the logits s = x.U, t = x.V (U, V the
+ *    folded att . W vectors) use the same 3-term f16 split on MFMA; softmax,
  *    aggregation and accumulation are fp32.  A bf16 x is converted exactly on
  *    load, so the result is the fp32 forward of the bf16-rounded features.
  *  - Graph layout: ``edge_index`` is the reference's COO ``int64 [2, E]``
@@ -251,12 +252,14 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int in_fea
  * GFD_STAGE_TILES (the tile kernels of every destination class, reading the
  * merged hub rows from ws) or GFD_STAGE_ALL; split calls must pass the same ws.
  * The tile stage schedules destinations by the plan's classes: general (hub
- * rows, 5+ messages), light (2..4), lone (self loop only). */
+ * rows, 7+ messages), light (2..6 messages, GFD_LIGHT_MAX in gfd_common.h),
+ * lone (self loop only). */
 #define GFD_STAGE_HUBS 1
 #define GFD_STAGE_TILES 2
 #define GFD_STAGE_ALL 3
 /* single tile classes (profiling splits; the union equals GFD_STAGE_TILES):
- * general (k_mid / k_fused), light (k_stream), lone (k_lone) */
+ * general (k_stream<general>, or k_fused for F > 168), light
+ * (k_stream<light>), lone (k_lone) */
 #define GFD_STAGE_TILES_GENERAL 4
 #define GFD_STAGE_TILES_LIGHT 8
 #define GFD_STAGE_TILES_LONE 16

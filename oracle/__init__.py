@@ -4,7 +4,7 @@ model wiring.  TEST INFRASTRUCTURE ONLY -- imported by ``tests/``,
 the product package ``gfd``.  See oracle/gatconv_ref.py for the parity status.
 """
 from .gatconv_ref import (GATConvRef, gatconv_forward, gatconv_forward_chunked,  # noqa: F401
-                          gatconv_forward_at, gatconv_forward_sampled,
+                          gatconv_forward_at, gatconv_forward_sampled, gatconv_grads_chunked,
                           remove_then_add_self_loops, segment_softmax, glorot_)
 from .models_ref import GATRef, TemporalGNNRef  # noqa: F401
 from .ingest_ref import process_ref  # noqa: F401

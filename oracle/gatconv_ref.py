@@ -212,6 +212,61 @@ class gatconv_forward_sampled:  # noqa: N801 (a namespace: prepare once, run man
         return out + bias if bias is not None else out
 
 
+def gatconv_grads_chunked(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor,
+                          weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor,
+                          bias: torch.Tensor, grad_out: torch.Tensor, heads: int = 8,
+                          chunk_edges: int = 2_000_000, dtype=torch.float32) -> dict:
+    """Gradients of ``sum(out * grad_out)`` for the PyG-dataflow forward on a
+    destination-sorted CSR (self loops in), with the backward that autograd
+    takes through it (train.py:142) -- at sizes where the ``[E', H, C]``
+    message tensor does not fit: h = x W^T is computed once for every node;
+    destination chunks of <= ``chunk_edges`` messages then run the logits,
+    segment softmax and aggregation under autograd with the gathered h rows as
+    leaves, and their row gradients are summed into dh ``[N, H*C]``; finally
+    grad_W = dh^T x and grad_x = dh W.  att_src / att_dst / bias gradients
+    accumulate through autograd chunk by chunk.  Returns a dict of CPU tensors
+    (x, weight, att_src, att_dst, bias) in ``dtype`` (float64: a reference
+    whose own rounding is negligible next to the fp32 tolerance at N ~ 1e6+)."""
+    N, Fin = x.shape
+    H = heads
+    C = weight.size(0) // H
+    x = x.to(dtype)
+    W = weight.detach().to(dtype)
+    with torch.no_grad():
+        h_all = x @ W.t()                                   # [N, H*C]
+    a_s = att_src.detach().reshape(1, H, C).to(dtype).clone().requires_grad_(True)
+    a_d = att_dst.detach().reshape(1, H, C).to(dtype).clone().requires_grad_(True)
+    b = bias.detach().to(dtype).clone().requires_grad_(True)
+    dh = torch.zeros_like(h_all)
+    rp = rowptr.long()
+    col = col.long()
+    start = 0
+    while start < N:
+        e0 = int(rp[start])
+        k = int(torch.searchsorted(rp, torch.tensor([e0 + chunk_edges]), right=True).item()) - 1
+        stop = min(N, max(start + 1, k))
+        e1 = int(rp[stop])
+        j = col[e0:e1]
+        seg = torch.repeat_interleave(torch.arange(stop - start),
+                                      (rp[start + 1:stop + 1] - rp[start:stop]))
+        dsts = torch.arange(start, stop)
+        rows, inv = torch.unique(torch.cat([j, dsts]), return_inverse=True)
+        hr = h_all[rows].view(-1, H, C).clone().requires_grad_(True)
+        jl, il = inv[:j.numel()], inv[j.numel():]
+        a_src = (hr * a_s).sum(-1)
+        a_dst = (hr * a_d).sum(-1)
+        logit = F.leaky_relu(a_src[jl] + a_dst[il][seg], NEG_SLOPE)
+        alpha = segment_softmax(logit, seg, stop - start)
+        agg = torch.zeros((stop - start, H, C), dtype=hr.dtype).index_add(
+            0, seg, alpha.unsqueeze(-1) * hr[jl])
+        out = agg.mean(dim=1) + b
+        (out * grad_out[start:stop].to(dtype)).sum().backward()
+        dh.index_add_(0, rows, hr.grad.reshape(rows.numel(), H * C))
+        start = stop
+    return {"x": dh @ W, "weight": dh.t() @ x, "att_src": a_s.grad.reshape(att_src.shape),
+            "att_dst": a_d.grad.reshape(att_dst.shape), "bias": b.grad}
+
+
 def glorot_(t: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:
     """PyG ``inits.glorot``: U(-a, a), a = sqrt(6 / (fan_in + fan_out)) over the last two dims."""
     a = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))

@@ -6,7 +6,7 @@ the tile stage's assumptions.
   4 GiB are gathered -- the max|x| single-scale path, the class-scheduled
   tile stage): >= 512 sampled destinations (the 16 largest hubs, the 64
   highest node ids, 64 slots of each class, random) against the oracle, and
-  the same through a 2-rank destination-sharded split.
+  the same through 2- and 8-rank destination-sharded splits.
 * C5's bf16 features (fp32 oracle on the bf16-rounded x).
 * Heavy-tailed features (max |x| = 1e6, 1e9), NaN-filled row padding with
   the last row ending at the end of its allocation, plans whose slot order is
@@ -77,28 +77,34 @@ def test_c4_bench_configuration_sampled_parity(c4):
     assert_close(out[dsts], _reference(s, dsts), what="C4 bench config, sampled")
 
 
-def test_c4_two_rank_dst_shards(c4):
-    """The destination-sharded split (ranks 0 and 1 of 2, run one after the
+@pytest.mark.parametrize("world", [2, 8])
+def test_c4_dst_shards(c4, world):
+    """The destination-sharded split (ranks 0..world-1, run one after the
     other on this GPU) at the bench's size: each rank's shard plan, the
-    all-rows logits and max|x|, and the shard's outputs."""
+    all-rows logits and max|x|, and the shard's outputs, against the oracle
+    at the sampled destinations and the rows around every shard boundary
+    (world 8: the 8-GPU form of the C4 bench)."""
     import bench
     from gfd import dist as gdist
     s = dict(c4)
     g = s["graph"]
     outs = []
-    for r in range(2):
-        s["spec"] = gdist.ShardSpec(g.rowptr, r, 2)
+    for r in range(world):
+        s["spec"] = gdist.ShardSpec(g.rowptr, r, world)
         s["shard"] = g.shard(s["spec"].dst_lo, s["spec"].dst_hi)
         layer = bench.Layer(s, DEV, 1)      # world 1: logits over all rows = the all-gather
         layer.step()
         torch.cuda.synchronize()
         outs.append((s["spec"], layer.out[:s["spec"].dst_hi - s["spec"].dst_lo].clone()))
+        del layer
     out = torch.cat([o for _, o in outs])
     assert out.shape[0] == g.num_nodes
-    lo1 = outs[1][0].dst_lo
-    edge = torch.arange(max(lo1 - 32, 0), min(lo1 + 32, g.num_nodes), device=DEV)
-    dsts = torch.unique(torch.cat([_sample(bench.Layer(c4, DEV, 1), c4), edge]))
-    assert_close(out[dsts], _reference(s, dsts), what="C4 2-rank shards, sampled")
+    edges = [torch.arange(max(sp.dst_lo - 16, 0), min(sp.dst_lo + 16, g.num_nodes), device=DEV)
+             for sp, _ in outs[1:]]
+    dsts = torch.unique(torch.cat([_sample(bench.Layer(c4, DEV, 1), c4)] + edges))
+    assert_close(out[dsts], _reference(s, dsts), what=f"C4 {world}-rank shards, sampled")
+    for k in [k for k in g._shards if k != (0, g.num_nodes)]:
+        del g._shards[k]
 
 
 def _small(N, E, F, seed, dtype=torch.float32, pitch=None):

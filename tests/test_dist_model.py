@@ -1,6 +1,7 @@
 """Model-level destination sharding (gfd.dist.model_forward_sharded; SURVEY.md
-§8e: layer 0 exchanges the [N, 16] logits, layers >= 1 all-gather the previous
-layer's [N, 64] output; BN / ReLU / residual fused into each shard's store).
+§8e: layer 0 exchanges the [N, 8] source logits, layers >= 1 all-gather the
+previous layer's [N, 64] output together with the next layer's source logits
+in one collective; BN / ReLU / residual fused into each shard's store).
 
 CPU (gloo, world 2 and 3): the orchestration -- collectives, shard bounds, the
 per-layer exchange and the epilogue arguments -- with the HIP stage functions
@@ -108,7 +109,7 @@ def _rank_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_model_sharded_orchestration_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -127,7 +128,7 @@ def test_model_sharded_orchestration_gloo(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_model_virtual_ranks_match_single_gpu(world):
     from gfd import dist as gdist, graph as ggraph
     from gfd.fused import bn_affine

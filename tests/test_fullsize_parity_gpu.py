@@ -1,0 +1,167 @@
+"""GPU parity at the sizes the bench quotes but round 2 never checked
+("Next round" item 1).
+
+* C5 exactly as bench.py builds and times it (bench.setup: 50M nodes / 500M
+  input edges, bf16 x at row pitch 168, so element indices reach 8.4e9 > 2^32;
+  ~1.1M hub chunks, E' = 550M) through bench.Layer -- the fused logits + lone
+  pass, hubs, general and light kernels -- compared with the oracle on >= 512
+  sampled destinations: hubs spread over the hub ranks (the largest two
+  included), destinations whose source rows lie past element 2^32, 64 slots of
+  each class, random rows.  The same sample through 8 destination shards run
+  one after another on this GPU (the 8-GPU form of C5, minus the all-gather,
+  which the logits over every row replace).
+* The backward (gat.py:80 under loss.backward(), train.py:142) on a C4-shaped
+  graph at 2M nodes / 10M edges (hubs of thousands of messages, source hubs of
+  the CSC pass, x at pitch 168): grad_W, grad_att_src, grad_att_dst,
+  grad_bias and grad_x against oracle.gatconv_grads_chunked (the PyG-dataflow
+  autograd run in destination chunks).
+Tolerances: forward 1e-4 + 1e-4 |ref| (north_star); gradients 1e-4 max|ref|.
+"""
+import pytest
+import torch
+
+from _util import assert_close, assert_close_scaled
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+H, C = 8, 64
+ROW_PAST_2_32 = (2 ** 32) // 168 + 1     # first node whose bf16 row starts past element 2^32
+
+
+def _reference(s, dsts, max_msgs=1_500_000):
+    """oracle.gatconv_forward_sampled over groups of destinations holding at
+    most ``max_msgs`` messages each (host memory stays a few GB at C5)."""
+    from oracle import gatconv_forward_sampled
+    rp = s["graph"].rowptr
+    deg = (rp[dsts.long() + 1] - rp[dsts.long()]).long().cpu()
+    outs, i = [], 0
+    W, a_s, a_d, b = (s["W"].cpu(), s["a_s"].cpu(), s["a_d"].cpu(), s["bias"].cpu())
+    while i < dsts.numel():
+        j, m = i, 0
+        while j < dsts.numel() and (j == i or m + int(deg[j]) <= max_msgs):
+            m += int(deg[j])
+            j += 1
+        sub = gatconv_forward_sampled.prepare(s["x"], rp, s["graph"].col, dsts[i:j])
+        outs.append(gatconv_forward_sampled.run(sub, W, a_s, a_d, b))
+        print(f"[oracle] destinations {i}..{j} of {dsts.numel()} ({m} messages)", flush=True)
+        i = j
+    return torch.cat(outs)
+
+
+def _c5_sample(layer, s):
+    g = s["graph"]
+    plan = layer.plan
+    N = g.num_nodes
+    deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
+    light_b, lone_b = plan.classes()
+    order = plan.row_order.long()
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    by_deg = torch.argsort(deg, descending=True)
+    pick = [by_deg[torch.tensor([0, 1, 10, 100, 1000, 10_000, 100_000, 250_000], device=DEV)],
+            torch.arange(N - 32, N, device=DEV),
+            torch.randint(ROW_PAST_2_32, N, (64,), generator=gen, device=DEV)]
+    for lo, hi in ((0, light_b), (light_b, lone_b), (lone_b, N)):
+        pick.append(order[torch.randint(lo, hi, (64,), generator=gen, device=DEV)])
+    pick.append(torch.randint(0, N, (256,), generator=gen, device=DEV))
+    # destinations that gather a source row past element 2^32 of x
+    e = torch.randint(0, g.num_messages, (4096,), generator=gen, device=DEV)
+    far = e[g.col[e].long() >= ROW_PAST_2_32][:64]
+    pick.append(torch.searchsorted(g.rowptr, far.to(torch.int32), right=True).long() - 1)
+    return torch.unique(torch.cat(pick))
+
+
+@pytest.fixture(scope="module")
+def c5():
+    import bench
+    s = bench.setup(DEV, 50_000_000, 500_000_000, 166, dtype=torch.bfloat16)
+    s["bias"] = torch.randn(C, generator=torch.Generator().manual_seed(2)).to(DEV) * 0.1
+    yield s
+    del s
+    torch.cuda.empty_cache()
+
+
+def test_c5_full_size_sampled_parity(c5):
+    import bench
+    s = c5
+    assert s["ldx"] == 168 and s["x"].dtype == torch.bfloat16
+    assert s["xbuf"].numel() > 2 ** 32                      # element indices past 2^32
+    layer = bench.Layer(s, DEV, 1)
+    light_b, lone_b = layer.plan.classes()
+    assert 0 < light_b < lone_b < s["graph"].num_nodes
+    assert layer.plan.num_chunks > 1_000_000                 # the C5 hub-chunk regime
+    layer.step()
+    torch.cuda.synchronize()
+    out = layer.out
+    assert torch.isfinite(out).all()
+    dsts = _c5_sample(layer, s)
+    assert dsts.numel() >= 512
+    # the sample really gathers rows past 2^32 elements
+    g = s["graph"]
+    rp = g.rowptr.long()
+    hit = sum(int((g.col[rp[d]:rp[d + 1]].long() >= ROW_PAST_2_32).any()) for d in dsts[:64].tolist())
+    assert hit > 0
+    c5["_dsts"] = dsts
+    c5["_out"] = out[dsts].cpu()
+    del layer
+    torch.cuda.empty_cache()
+    c5["_ref"] = _reference(s, dsts)
+    assert_close(c5["_out"], c5["_ref"], what="C5 bench config, sampled")
+
+
+def test_c5_eight_destination_shards(c5):
+    """8 destination shards (gfd.dist.ShardSpec balanced by messages, each with
+    its own plan and the unfused lone kernel) run one after another: every
+    sampled destination's row from its owner against the oracle."""
+    import bench
+    from gfd import dist as gdist
+    s = dict(c5)
+    g = s["graph"]
+    dsts, ref = c5.get("_dsts"), c5.get("_ref")
+    if dsts is None or ref is None:
+        pytest.skip("needs test_c5_full_size_sampled_parity's sample")
+    got = torch.empty((dsts.numel(), C))
+    seen = torch.zeros(dsts.numel(), dtype=torch.bool)
+    for r in range(8):
+        spec = gdist.ShardSpec(g.rowptr, r, 8)
+        s["spec"] = spec
+        s["shard"] = g.shard(spec.dst_lo, spec.dst_hi)
+        layer = bench.Layer(s, DEV, 1)
+        layer.step()
+        torch.cuda.synchronize()
+        mine = (dsts >= spec.dst_lo) & (dsts < spec.dst_hi)
+        got[mine.cpu()] = layer.out[dsts[mine] - spec.dst_lo].cpu()
+        seen |= mine.cpu()
+        del layer
+        g._shards.clear()
+        torch.cuda.empty_cache()
+    assert seen.all()
+    assert_close(got, ref, what="C5 8 shards, sampled")
+
+
+def test_backward_c4_shaped_2m_nodes():
+    import bench
+    from gfd.nn import gat_conv
+    from oracle import gatconv_grads_chunked
+    s = bench.setup(DEV, 2_000_000, 10_000_000, 166)
+    g = s["graph"]
+    deg = (g.rowptr[1:] - g.rowptr[:-1])
+    assert int(deg.max()) > 1000                            # hubs: many 256-message chunks
+    csc = g.csc()
+    assert csc.plan.num_hubs > 0                            # source hubs (k_bwd_src chunks)
+    gen = torch.Generator().manual_seed(6)
+    bias = (torch.randn(C, generator=gen) * 0.1).to(DEV)
+    x = s["x"].detach().requires_grad_(True)                 # pitch-168 view
+    W = s["W"].clone().requires_grad_(True)
+    a_s = s["a_s"].clone().requires_grad_(True)
+    a_d = s["a_d"].clone().requires_grad_(True)
+    b = bias.clone().requires_grad_(True)
+    gout = torch.randn((g.num_nodes, C), generator=gen)
+    out = gat_conv(x, g, W, a_s, a_d, b, training=True)
+    out.backward(gout.to(DEV))
+    torch.cuda.synchronize()
+    got = {"x": x.grad.cpu(), "weight": W.grad.cpu(), "att_src": a_s.grad.cpu(),
+           "att_dst": a_d.grad.cpu(), "bias": b.grad.cpu()}
+    ref = gatconv_grads_chunked(s["x"].detach().cpu(), g.rowptr.cpu(), g.col.cpu(),
+                                s["W"].cpu(), s["a_s"].cpu(), s["a_d"].cpu(), bias.cpu(), gout)
+    for k in ("weight", "att_src", "att_dst", "bias", "x"):
+        assert_close_scaled(got[k].reshape(ref[k].shape), ref[k], what=f"2M-node backward grad_{k}")

@@ -88,3 +88,23 @@ def test_edgecase_fixture_covers_what_it_claims(golden):
     assert len(np.unique(pairs)) < len(pairs)               # duplicates
     full = remove_then_add_self_loops(torch.from_numpy(ei), N)
     assert full.shape[1] == ei.shape[1] - (ei[0] == ei[1]).sum() + N
+
+
+@pytest.mark.parametrize("fixture,case", [("gatconv_edgecases.npz", "base"),
+                                          ("gatconv_f166.npz", "pl")])
+def test_chunked_backward_oracle_matches_golden_grads(golden, fixture, case):
+    """oracle.gatconv_grads_chunked (the large-graph backward checker: h once,
+    destination chunks under autograd, dh summed) against the fixture grads of
+    the plain PyG-dataflow autograd, with chunks small enough to split hubs'
+    neighbourhoods across many chunk boundaries."""
+    from oracle import gatconv_grads_chunked
+    from _util import csr_cpu
+    arr = golden(fixture)
+    t = lambda k: torch.from_numpy(arr[f"{case}.{k}"])  # noqa: E731
+    x = t("x")
+    rp, col = csr_cpu(t("edge_index"), x.shape[0])
+    r = gatconv_grads_chunked(x, rp, col, t("weight"), t("att_src"), t("att_dst"), t("bias"),
+                              t("grad_out"), chunk_edges=997)
+    for k in ("x", "weight", "att_src", "att_dst", "bias"):
+        assert_close_scaled(r[k].reshape(arr[f"{case}.grad_{k}"].shape), arr[f"{case}.grad_{k}"],
+                            rtol=2e-6, what=f"{fixture}/{case} grad_{k}")

@@ -135,3 +135,14 @@ def test_loader_training_step_on_sampled_batches():
             break
     assert seen == 4 * 256
     assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+def test_batch_seeds_do_not_collide_across_fields():
+    """(seed, epoch, batch) -> draw stream: tuples that overlapping bit fields
+    would merge (batch 2^20 of epoch e vs batch 0 of e + 1; epochs >= 2^12 vs
+    the user seed) get distinct streams."""
+    from gfd.sampler import batch_seed
+    assert batch_seed(0, 0, 2 ** 20) != batch_seed(0, 1, 0)
+    assert batch_seed(0, 2 ** 12, 0) != batch_seed(1, 0, 0)
+    seen = {batch_seed(s, e, b) for s in range(3) for e in range(20) for b in range(200)}
+    assert len(seen) == 3 * 20 * 200
