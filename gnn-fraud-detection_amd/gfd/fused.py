@@ -8,7 +8,9 @@
   path writes the GATConv output, then BN, ReLU and the residual add each
   read and write [N, 64] again).
 * ``gru_head`` -- the TemporalGNN head (tgn.py:108-111): GRUCell(h, h0) +
-  Linear in one kernel (``gfd_gru_head``).
+  Linear in one kernel (``gfd_gru_head``); ``tgn_head_train`` -- the same
+  head in training mode, forward and backward on the device
+  (``gfd_gru_head_bwd`` + ``gfd_atb``).
 
 * ``train_body`` -- the same layer body in training mode after the GATConv:
   residual + dropout(relu(BatchNorm1d(y))) with batch statistics, as one
@@ -110,6 +112,86 @@ def gru_head(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,
               w_o.data_ptr(), _lib.ptr(b_o), O, h_new.data_ptr(), out.data_ptr(),
               _lib.stream_handle(dev))
     return out, h_new
+
+
+class _GRUHeadTrain(torch.autograd.Function):
+    """(out, h_new) = (Linear(GRUCell(h, h0)), GRUCell(h, h0)) with both
+    directions on the device: forward = gfd_gru_head (the inference kernel:
+    gates on fp32 MFMA, nothing but h / h0 / h_new kept), backward =
+    gfd_gru_head_bwd (gates recomputed, gate gradients, grad_h / grad_h0) +
+    gfd_atb for the six weight / bias gradients (deterministic sums)."""
+
+    @staticmethod
+    def forward(ctx, h, h0, w_ih, b_ih, w_hh, b_hh, w_o, b_o):
+        dev = h.device
+        N = h.size(0)
+        O = w_o.size(0)
+        h_new = torch.empty((N, C), dtype=torch.float32, device=dev)
+        out = torch.empty((N, O), dtype=torch.float32, device=dev)
+        _lib.call("gfd_gru_head", h.data_ptr(), N, C, h.stride(0), w_ih.data_ptr(), _lib.ptr(b_ih),
+                  w_hh.data_ptr(), _lib.ptr(b_hh), _lib.ptr(h0),
+                  h0.stride(0) if h0 is not None else 0, w_o.data_ptr(), _lib.ptr(b_o), O,
+                  h_new.data_ptr(), out.data_ptr(), _lib.stream_handle(dev))
+        ctx.save_for_backward(h, h0, w_ih, b_ih, w_hh, b_hh, w_o, b_o, h_new)
+        return out, h_new
+
+    @staticmethod
+    def backward(ctx, g_out, g_hnew):
+        h, h0, w_ih, b_ih, w_hh, b_hh, w_o, b_o, h_new = ctx.saved_tensors
+        dev = h.device
+        N, O = h.size(0), w_o.size(0)
+        lib = _lib.load()
+        stream = _lib.stream_handle(dev)
+        g_out = (g_out if g_out is not None else torch.zeros((N, O), device=dev)).float().contiguous()
+        g_hnew = g_hnew.float().contiguous() if g_hnew is not None else None
+        grad_h = torch.empty((N, C), dtype=torch.float32, device=dev)
+        grad_h0 = torch.empty((N, C), dtype=torch.float32, device=dev) if h0 is not None else None
+        gi = torch.empty((N, 3 * C), dtype=torch.float32, device=dev)
+        gh = torch.empty_like(gi)
+        _lib.call("gfd_gru_head_bwd", h.data_ptr(), N, C, h.stride(0), w_ih.data_ptr(),
+                  _lib.ptr(b_ih), w_hh.data_ptr(), _lib.ptr(b_hh), _lib.ptr(h0),
+                  h0.stride(0) if h0 is not None else 0, w_o.data_ptr(), O, g_out.data_ptr(),
+                  _lib.ptr(g_hnew), grad_h.data_ptr(), _lib.ptr(grad_h0), gi.data_ptr(),
+                  gh.data_ptr(), stream)
+        ws = _ws(lib.gfd_atb_workspace_size(N, 3 * C), dev)
+
+        def atb(A, m, B):
+            wgt = torch.empty((m, C), dtype=torch.float32, device=dev)
+            col = torch.empty((m,), dtype=torch.float32, device=dev)
+            _lib.call("gfd_atb", A.data_ptr(), A.stride(0), m, _lib.ptr(B),
+                      B.stride(0) if B is not None else C, N, wgt.data_ptr(), col.data_ptr(),
+                      ws.data_ptr(), ws.numel(), stream)
+            return wgt, col
+
+        g_wih, g_bih = atb(gi, 3 * C, h)
+        if h0 is not None:
+            g_whh, g_bhh = atb(gh, 3 * C, h0)
+        else:                                   # h0 = 0: no W_hh product, only b_hh
+            g_whh = torch.zeros_like(w_hh)
+            g_bhh = atb(gh, 3 * C, h)[1]
+        g_wo, g_bo = atb(g_out, O, h_new)
+        return (grad_h, grad_h0, g_wih, g_bih if b_ih is not None else None, g_whh,
+                g_bhh if b_hh is not None else None, g_wo, g_bo if b_o is not None else None)
+
+
+def tgn_head_train(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,
+                   h0: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Training form of ``gru_head``: (lin(GRUCell(h, h0)), GRUCell(h, h0)) as
+    one autograd Function over gfd_gru_head / gfd_gru_head_bwd / gfd_atb
+    (tgn.py:108-111 under loss.backward(), train.py:142)."""
+    if gru.hidden_size != C or gru.input_size != C or not gru.bias:
+        raise NotImplementedError("gfd tgn_head_train: GRUCell(64, 64) with biases")
+    x = h if h.dtype == torch.float32 else h.float()
+    x = x if x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 \
+        else x.contiguous()
+    if h0 is not None:
+        h0 = h0.float() if h0.dtype != torch.float32 else h0
+        h0 = h0 if h0.stride(1) == 1 and h0.stride(0) % 4 == 0 and h0.data_ptr() % 16 == 0 \
+            else h0.contiguous()
+    b_o = lin.bias
+    return _GRUHeadTrain.apply(x, h0, gru.weight_ih.contiguous(), gru.bias_ih,
+                               gru.weight_hh.contiguous(), gru.bias_hh, lin.weight.contiguous(),
+                               b_o)
 
 
 class _BNReluDropout(torch.autograd.Function):

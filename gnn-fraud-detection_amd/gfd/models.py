@@ -13,7 +13,8 @@ under no_grad) each layer is one fused call (BN folded into the GATConv store
 epilogue, ``gfd.fused.gat_layer``) and the TemporalGNN head is one kernel
 (``gfd.fused.gru_head``); in training the body after each GATConv (batch-
 statistics BN, ReLU, dropout, residual) is one autograd Function over two
-kernels each way (``gfd.fused.train_body``).
+kernels each way (``gfd.fused.train_body``), and the TemporalGNN head is one
+too (``gfd.fused.tgn_head_train``: GRUCell + Linear forward and backward).
 
 ``forward_snapshots`` is config C3: the TGN forward over per-time-step
 snapshots (h0 = 0 per step, tgn.py:88-89).  Elliptic edges never cross time
@@ -126,6 +127,11 @@ class TemporalGNN(_GATStack):
         if self._fused():
             from . import fused
             return fused.gru_head(self.gru, self.out, h, hidden_state)
+        if h.is_cuda and self.gru.bias and self.out.in_features == self.hidden_channels == 64:
+            # training / autograd: GRUCell + Linear forward and backward on the
+            # device (gfd.fused.tgn_head_train); h0 = None is the reference's zeros
+            from . import fused
+            return fused.tgn_head_train(self.gru, self.out, h, hidden_state)
         if hidden_state is None:
             hidden_state = x.new_zeros((x.size(0), self.hidden_channels))
         new_hidden = self.gru(h, hidden_state)

@@ -364,6 +364,32 @@ gfd_status gfd_gru_head(const float* h, int64_t rows, int channels, int64_t h_st
                         const float* w_out, const float* b_out, int out_channels, float* h_new,
                         float* out, gfd_stream_t stream);
 
+/* Training backward of the same head (autograd of tgn.py:108-111 at
+ * loss.backward(), train.py:142), given grad_out [rows, out_channels] and
+ * grad_hnew (nullable) [rows, C] = dL/dh_new: recomputes the gates exactly as
+ * gfd_gru_head does and writes grad_h [rows, C] = gi W_ih, grad_h0 [rows, C]
+ * (required when h0 != NULL) = gh W_hh + dL/dh' z, and the gate gradients
+ * gates_i = [dr | dz | dn] and gates_h = [dr | dz | dn r] ([rows, 3C] each;
+ * pre-activation gradients of the x side and the h side) for gfd_atb:
+ * grad_W_ih = gates_i^T h, grad_b_ih = colsum(gates_i), grad_W_hh = gates_h^T
+ * h0, grad_b_hh = colsum(gates_h), grad_W_out = grad_out^T h_new, grad_b_out
+ * = colsum(grad_out).  Same alignment rules as gfd_gru_head (w_hh required). */
+gfd_status gfd_gru_head_bwd(const float* h, int64_t rows, int channels, int64_t h_stride,
+                            const float* w_ih, const float* b_ih, const float* w_hh,
+                            const float* b_hh, const float* h0, int64_t h0_stride,
+                            const float* w_out, int out_channels, const float* grad_out,
+                            const float* grad_hnew, float* grad_h, float* grad_h0,
+                            float* gates_i, float* gates_h, gfd_stream_t stream);
+
+/* Weight gradient of a row-wise linear map: out[m][n] = sum_r A[r][m] B[r][n]
+ * (m < M <= 192, n < 64; A row stride lda >= M, B row stride ldb >= 64) and
+ * colsum[m] = sum_r A[r][m] (nullable), fp32 MFMA, deterministic (fixed-order
+ * split over row slabs).  Replaces the autograd weight-gradient GEMMs of the
+ * TGN head's GRUCell and Linear (tgn.py:108-111). */
+size_t gfd_atb_workspace_size(int64_t rows, int m);
+gfd_status gfd_atb(const float* A, int64_t lda, int m, const float* B, int64_t ldb, int64_t rows,
+                   float* out, float* colsum, void* ws, size_t ws_bytes, gfd_stream_t stream);
+
 /* gfd_gat_aggregate_ex followed by the inference epilogue (ep nullable); the
  * residual rows are indexed like out (destination dst_offset + i at row i).
  * The destination-sharded model forward (gfd.dist) runs every layer through

@@ -264,7 +264,7 @@ def gatconv_grads_chunked(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tens
         dh.index_add_(0, rows, hr.grad.reshape(rows.numel(), H * C))
         start = stop
     return {"x": dh @ W, "weight": dh.t() @ x, "att_src": a_s.grad.reshape(att_src.shape),
-            "att_dst": a_d.grad.reshape(att_dst.shape), "bias": b.grad}
+            "att_dst": a_d.grad.reshape(att_dst.shape), "bias": b.grad, "dh": dh}
 
 
 def glorot_(t: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:

@@ -145,6 +145,33 @@ def train_grads():
     save("gat3_train_grads.npz", **arrays)
 
 
+def tgn_train_grads():
+    """One training step of the reference's TemporalGNN (train.py:115-121 runs
+    the same loop for --model_type tgn): tgn.py forward with h0 = 0 (the
+    GRUCell(h, 0) + Linear head, tgn.py:88-89, 108-111), BCE(pos_weight=50)
+    on the labelled nodes, backward.  Dropout 0 so the step is deterministic."""
+    g = synth.elliptic_like(num_nodes=1000, num_edges=1150, num_steps=49, num_features=165, seed=4)
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    ei = torch.from_numpy(g["edge_index"])
+    y = torch.from_numpy(g["y"])
+    sd = load_ckpt("tgn_model.pt")
+    tgn = build_model("tgn", sd, 165, dropout=0.0).train()
+    out, hidden = tgn(x, ei)                                      # train.py:117 (tgn branch)
+    mask = y != -1
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0]))
+    loss = crit(out[mask].squeeze(1), y[mask].float())
+    loss.backward()
+    arrays = {"x": g["x"], "edge_index": g["edge_index"], "y": g["y"],
+              "logits": out.detach().numpy(), "hidden": hidden.detach().numpy(),
+              "loss": np.array(loss.item(), dtype=np.float64), "grad_x": x.grad.numpy()}
+    arrays.update(sd_arrays(sd, "w."))
+    for name, p in tgn.named_parameters():
+        if name.endswith("lin_dst.weight"):
+            continue
+        arrays["grad." + name] = p.grad.numpy()
+    save("tgn3_train_grads.npz", **arrays)
+
+
 def single_layer_case(name, x, ei, seed, att_scale=1.0):
     gen = torch.Generator().manual_seed(seed)
     conv = GATConvRef(x.shape[1], 64, heads=8, concat=False, dropout=0.0)
@@ -198,7 +225,7 @@ def f166_powerlaw():
 
 
 if __name__ == "__main__":
-    elliptic_small()
-    train_grads()
-    edge_cases()
-    f166_powerlaw()
+    which = sys.argv[1:] or ["elliptic_small", "train_grads", "tgn_train_grads", "edge_cases",
+                             "f166_powerlaw"]
+    for fn in which:
+        globals()[fn]()

@@ -187,6 +187,75 @@ def test_gat_train_step_grads_match_reference(golden):
         assert_close_scaled(p.grad, arr["grad." + name], rtol=2e-4, atol=1e-5, what=f"grad {name}")
 
 
+def test_tgn_train_step_grads_match_reference(golden):
+    """The TemporalGNN training step (train.py:115-121, 139-142 for the tgn
+    model): GAT stack + GRUCell(h, 0) + Linear in training mode on the device
+    (gfd.fused.tgn_head_train: one kernel forward, one backward), BCE(pos_weight
+    = 50), backward -- every gradient against the reference's own tgn.py run."""
+    arr = golden("tgn3_train_grads.npz")
+    m = _model("tgn", arr, "w.", dropout=0.0).train()
+    x = torch.from_numpy(arr["x"]).to(DEV).requires_grad_(True)
+    ei = torch.from_numpy(arr["edge_index"]).to(DEV)
+    y = torch.from_numpy(arr["y"]).to(DEV)
+    out, hid = m(x, ei)
+    mask = y != -1
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0], device=DEV))
+    loss = crit(out[mask].squeeze(1), y[mask].float())
+    loss.backward()
+    assert_close(out, arr["logits"], what="tgn train logits")
+    assert_close(hid, arr["hidden"], what="tgn train hidden")
+    assert abs(loss.item() - float(arr["loss"])) <= 1e-4 * max(1.0, abs(float(arr["loss"])))
+    assert_close_scaled(x.grad, arr["grad_x"], rtol=2e-4, what="grad_x")
+    for name, p in m.named_parameters():
+        if name.endswith("lin_dst.weight"):
+            continue
+        assert_close_scaled(p.grad, arr["grad." + name], rtol=2e-4, atol=1e-5, what=f"grad {name}")
+
+
+def test_tgn_head_train_kernel_matches_autograd():
+    """gfd.fused.tgn_head_train (GRUCell + Linear forward and backward kernels)
+    against torch autograd of nn.GRUCell + nn.Linear in fp64, with and without
+    h0, with a gradient on the hidden output too, rows not a multiple of 16."""
+    from gfd.fused import tgn_head_train
+    torch.manual_seed(0)
+    gru = torch.nn.GRUCell(64, 64).to(DEV)
+    lin = torch.nn.Linear(64, 1).to(DEV)
+    for N, with_h0 in ((1000, False), (4099, True)):
+        h = torch.randn(N, 64, device=DEV, requires_grad=True)
+        h0 = torch.randn(N, 64, device=DEV, requires_grad=True) if with_h0 else None
+        go = torch.randn(N, 1, device=DEV)
+        gh = torch.randn(N, 64, device=DEV) * 0.1
+        out, hn = tgn_head_train(gru, lin, h, h0)
+        (out * go).sum().add_((hn * gh).sum()).backward()
+        got = {"h": h.grad.clone(), "w_ih": gru.weight_ih.grad.clone(),
+               "w_hh": gru.weight_hh.grad.clone(), "b_ih": gru.bias_ih.grad.clone(),
+               "b_hh": gru.bias_hh.grad.clone(), "w_o": lin.weight.grad.clone(),
+               "b_o": lin.bias.grad.clone()}
+        if with_h0:
+            got["h0"] = h0.grad.clone()
+        for p in list(gru.parameters()) + list(lin.parameters()):
+            p.grad = None
+        g64 = torch.nn.GRUCell(64, 64).double().to(DEV)
+        l64 = torch.nn.Linear(64, 1).double().to(DEV)
+        g64.load_state_dict({k: v.double() for k, v in gru.state_dict().items()})
+        l64.load_state_dict({k: v.double() for k, v in lin.state_dict().items()})
+        hr = h.detach().double().requires_grad_(True)
+        h0r = h0.detach().double().requires_grad_(True) if with_h0 else None
+        hnr = g64(hr, h0r)
+        outr = l64(hnr)
+        (outr * go.double()).sum().add_((hnr * gh.double()).sum()).backward()
+        assert_close(out, outr, what="tgn head out")
+        assert_close(hn, hnr, what="tgn head hidden")
+        want = {"h": hr.grad, "w_ih": g64.weight_ih.grad, "w_hh": g64.weight_hh.grad,
+                "b_ih": g64.bias_ih.grad, "b_hh": g64.bias_hh.grad, "w_o": l64.weight.grad,
+                "b_o": l64.bias.grad}
+        if with_h0:
+            want["h0"] = h0r.grad
+        for k in want:
+            assert_close_scaled(got[k], want[k], rtol=1e-5, what=f"N={N} h0={with_h0} grad {k}")
+        h.grad = None
+
+
 def test_state_dict_roundtrip_keeps_lin_alias(golden):
     arr = golden("elliptic_small.npz")
     m = _model("gat", arr, "gat.")

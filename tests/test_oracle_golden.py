@@ -66,6 +66,27 @@ def test_oracle_train_grads_match_reference(golden):
             assert_close_scaled(p.grad, arr["grad." + name], rtol=1e-6, atol=1e-6, what=name)
 
 
+def test_oracle_tgn_train_grads_match_reference(golden):
+    """The TemporalGNN training step (tgn.py forward with h0 = 0, BCE(pos_weight
+    = 50) on y != -1, backward) of the oracle wiring against the reference's own
+    tgn.py run (tgn3_train_grads.npz)."""
+    arr = golden("tgn3_train_grads.npz")
+    m = _ref_model(TemporalGNNRef, arr, "w.", dropout=0.0).train()
+    x = torch.from_numpy(arr["x"]).requires_grad_(True)
+    ei, y = torch.from_numpy(arr["edge_index"]), torch.from_numpy(arr["y"])
+    out, hid = m(x, ei)
+    mask = y != -1
+    loss = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0]))(
+        out[mask].squeeze(1), y[mask].float())
+    loss.backward()
+    assert abs(loss.item() - float(arr["loss"])) < 1e-6 * max(1, abs(float(arr["loss"])))
+    assert_close(hid, arr["hidden"], atol=1e-6, rtol=1e-6, what="hidden")
+    assert_close_scaled(x.grad, arr["grad_x"], rtol=1e-6, what="grad_x")
+    for name, p in m.named_parameters():
+        if not name.endswith("lin_dst.weight"):
+            assert_close_scaled(p.grad, arr["grad." + name], rtol=1e-6, atol=1e-6, what=name)
+
+
 @pytest.mark.parametrize("fixture,case", [("gatconv_edgecases.npz", "base"),
                                           ("gatconv_edgecases.npz", "scale100"),
                                           ("gatconv_f166.npz", "pl")])
