@@ -8,9 +8,10 @@
 //                  light slots    k_stream<LIGHT = true>
 //                  lone slots     k_lone    (gfd_lone.hip)
 //                otherwise        k_fused   (gfd_fused.hip)
-// Classes come from the plan's class_split (gfd_plan_desc); with dropout, or
-// no class split, every slot goes to the general kernel.  No runtime switch
-// changes what a call computes.
+// Classes come from the plan's class_split (gfd_plan_desc); with no class
+// split every slot goes to the general kernel; with dropout the lone slots go
+// to the light kernel (per-head masks).  No runtime switch changes what a
+// call computes.
 #include <map>
 #include <mutex>
 #include <utility>
@@ -81,11 +82,13 @@ gfd_status tiles_impl(const AggArgs& a, const PackLayout& L, hipStream_t stream)
     if (s == GFD_ERR_UNSUPPORTED) return launch_fused(a, L, stream);
     if (s != GFD_OK) return s;
   }
-  if (!p.class_split || a.dp > 0.f) return GFD_OK;  // the general kernel took every tile
-  // lone slots need 16-B aligned rows; otherwise the light kernel runs to the end
+  if (!p.class_split) return GFD_OK;  // the general kernel took every tile
+  // lone slots need 16-B aligned rows and no dropout (k_lone projects with the
+  // head mean; a dropout mask differs per head); otherwise the light kernel
+  // runs to the end and takes them as one-message slots
   const uintptr_t base = reinterpret_cast<uintptr_t>(a.x);
   const int eb = a.xdt == GFD_DTYPE_BF16 ? 2 : 4;
-  const bool lone = base % 16 == 0 && (a.ldx * eb) % 16 == 0 && L.KB <= 6;
+  const bool lone = base % 16 == 0 && (a.ldx * eb) % 16 == 0 && L.KB <= 6 && a.dp == 0.f;
   if (cls & kLightBit) {
     const gfd_status s = launch_light(a, L, !lone, stream);
     if (s != GFD_OK) return s;  // the class split promised a light kernel for this F

@@ -158,12 +158,15 @@ __device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[k
   else fma_k<KF, kLightMax>(z, xv, p);
 }
 
-// A slot with at most kLightMax messages (all rows prefetched), not a hub, no
-// dropout: straight-line code, the softmax sum and reciprocal independent of
-// the FMA block.  kmax: messages to run (wave-uniform, >= n).
+// A slot with at most kLightMax messages (all rows prefetched), not a hub
+// (with dropout also the self-loop-only slots: their heads are masked one by
+// one, so the head-mean shortcut of k_lone does not apply): straight-line
+// code, the softmax sum and reciprocal independent of the FMA block.  kmax:
+// messages to run (wave-uniform, >= n).
 template <int KF>
 __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLightMax>& q, int kmax,
-                                         float slope, int Fp, float* __restrict__ stats,
+                                         float slope, float dp, uint64_t seed, int Fp,
+                                         float* __restrict__ stats,
                                          _Float16* __restrict__ zh, _Float16* __restrict__ zl,
                                          float* __restrict__ rsc, int* __restrict__ rid, int r,
                                          int erg, int lane) {
@@ -183,17 +186,24 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLight
     sr[8] = l;
   }
   const float inv = __builtin_amdgcn_rcpf(l + kSoftmaxEps);
+  // training: dropout on alpha after the softmax (the statistics above are the
+  // undropped ones), the counter-based mask of (seed, CSR position, head) that
+  // the general / hub kernels and the backward use
+  float pd = p;
+  if (__builtin_expect(dp > 0.f, 0))  // kernel-uniform
+    pd = dropout_keep(seed, uint32_t(d.y + kk), uint32_t(lane & 7), dp) ? p * (1.0f / (1.0f - dp))
+                                                                        : 0.f;
   f32x2 z[4][KF];
   f16x8 hi[KF], lo[KF];
   int er = erg;
   if (erg != 127) {
     // one scale for every row: fold 1 / (sum + eps) and 2^erg into the
     // weights, so z comes out normalised and scaled and only needs the split
-    const float ps = p * (inv * ldexpf(1.0f, erg));
+    const float ps = pd * (inv * ldexpf(1.0f, erg));
     light_fma<KF>(z, q.xv, ps, kmax);
     split_zrow<KF>(z, hi, lo);
   } else {
-    light_fma<KF>(z, q.xv, p, kmax);
+    light_fma<KF>(z, q.xv, pd, kmax);
     er = pack_zrow<KF>(z, inv, erg, hi, lo);
   }
   write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
@@ -421,10 +431,10 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     if constexpr (LIGHT) {
       const int4 da = uni4(rg[r0].d), db = uni4(rg[r1].d);
       const int kmax = max(da.z - da.y, db.z - db.y);  // wave-uniform
-      sl_light<KF>(da, d0, kmax, slope, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg,
-                   lane);
-      sl_light<KF>(db, d1, kmax, slope, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg,
-                   lane);
+      sl_light<KF>(da, d0, kmax, slope, dp, seed, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid,
+                   r0, erg, lane);
+      sl_light<KF>(db, d1, kmax, slope, dp, seed, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid,
+                   r1, erg, lane);
     } else {
       sl_general<XT, KF>(rg + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
                          Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane);
@@ -583,8 +593,8 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
   int64_t grid = cu_count();
   if (grid > tiles) grid = tiles;
   const gfd_plan& p = a.plan;
-  // general: with dropout (no light / lone classes) or no class split, every tile
-  const int64_t* split = (!LIGHT && a.dp > 0.f) ? nullptr : p.class_split;
+  // general: the slots before the light class (every tile without a class split)
+  const int64_t* split = p.class_split;
   kern<<<int(grid), kSWaves * 64, lds, stream>>>(
       a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
       reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
@@ -631,7 +641,7 @@ gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t str
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
                         hipStream_t stream) {
   const gfd_plan& p = a.plan;
-  if (!p.slot_desc || !p.slot_cols || !p.class_split || a.dp > 0.f) return GFD_ERR_UNSUPPORTED;
+  if (!p.slot_desc || !p.slot_cols || !p.class_split) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
   return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, stream)
                                  : launch_stream_x<XF32, true>(a, L, to_end, stream);

@@ -215,7 +215,8 @@ class gatconv_forward_sampled:  # noqa: N801 (a namespace: prepare once, run man
 def gatconv_grads_chunked(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor,
                           weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor,
                           bias: torch.Tensor, grad_out: torch.Tensor, heads: int = 8,
-                          chunk_edges: int = 2_000_000, dtype=torch.float32) -> dict:
+                          chunk_edges: int = 2_000_000, dtype=torch.float32,
+                          kinks_from: Optional[torch.Tensor] = None) -> dict:
     """Gradients of ``sum(out * grad_out)`` for the PyG-dataflow forward on a
     destination-sorted CSR (self loops in), with the backward that autograd
     takes through it (train.py:142) -- at sizes where the ``[E', H, C]``
@@ -226,7 +227,16 @@ def gatconv_grads_chunked(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tens
     grad_W = dh^T x and grad_x = dh W.  att_src / att_dst / bias gradients
     accumulate through autograd chunk by chunk.  Returns a dict of CPU tensors
     (x, weight, att_src, att_dst, bias) in ``dtype`` (float64: a reference
-    whose own rounding is negligible next to the fp32 tolerance at N ~ 1e6+)."""
+    whose own rounding is negligible next to the fp32 tolerance at N ~ 1e6+),
+    plus ``dh`` = dL/dh [N, H*C].
+
+    ``kinks_from`` ([N, 2H] logits table s | t of the implementation under
+    test): the pre-activations s_j + t_i take those VALUES (the gradient path
+    is unchanged, a straight-through substitution), so LeakyReLU's derivative
+    -- 1 or the slope, a jump at 0 -- is decided on the same side as in the
+    implementation.  At 10^7+ messages some s_j + t_i lie within fp32
+    rounding of 0, where any two correct fp32 computations may pick
+    different sides and the gradient legitimately differs by O(1)."""
     N, Fin = x.shape
     H = heads
     C = weight.size(0) // H
@@ -255,7 +265,12 @@ def gatconv_grads_chunked(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tens
         jl, il = inv[:j.numel()], inv[j.numel():]
         a_src = (hr * a_s).sum(-1)
         a_dst = (hr * a_d).sum(-1)
-        logit = F.leaky_relu(a_src[jl] + a_dst[il][seg], NEG_SLOPE)
+        pre = a_src[jl] + a_dst[il][seg]
+        if kinks_from is not None:
+            kd = kinks_from[rows].to(dtype)
+            pre_d = kd[jl, :H] + kd[il, H:][seg]
+            pre = pre + (pre_d - pre).detach()
+        logit = F.leaky_relu(pre, NEG_SLOPE)
         alpha = segment_softmax(logit, seg, stop - start)
         agg = torch.zeros((stop - start, H, C), dtype=hr.dtype).index_add(
             0, seg, alpha.unsqueeze(-1) * hr[jl])

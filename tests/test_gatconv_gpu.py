@@ -296,6 +296,42 @@ def test_dropout_forward_backward_vs_oracle_with_same_mask():
     assert_close_scaled(b.grad, conv.bias.grad, what="dropout grad_bias")
 
 
+def test_dropout_all_classes_at_20k_nodes():
+    """The reference's training configuration (GATConv dropout=0.2, gat.py:39,
+    config.py:35) through the class-scheduled kernels: hubs, general, light
+    and the self-loop-only rows (which with dropout run in the light kernel:
+    per-head masks), forward and backward against the oracle with the device's
+    mask, on a 20k-node power-law graph where every class is populated."""
+    from gfd.nn import GATConvFunction
+    from oracle import gatconv_forward
+    _, graph = _gfd()
+    N, p, seed = 20000, 0.2, 4242
+    x, ei, conv = _random_case(N, 100000, 166, seed=21)
+    g = graph.get_graph(ei.to(DEV), N)
+    plan = g.plan()
+    light_b, lone_b = plan.classes()
+    assert plan.num_hubs > 0 and 0 < light_b < lone_b < N          # every class present
+    mask = _device_dropout_mask(ei, N, seed, p)
+    go = torch.randn(N, 64, generator=torch.Generator().manual_seed(3))
+    xr = x.clone().requires_grad_(True)
+    ref = gatconv_forward(xr, ei, conv.lin_src.weight, conv.att_src, conv.att_dst, conv.bias,
+                          alpha_mask=mask)
+    (ref * go).sum().backward()
+    xd = x.to(DEV).requires_grad_(True)
+    W = conv.lin_src.weight.detach().to(DEV).requires_grad_(True)
+    a_s = conv.att_src.detach().to(DEV).reshape(-1).requires_grad_(True)
+    a_d = conv.att_dst.detach().to(DEV).reshape(-1).requires_grad_(True)
+    b = conv.bias.detach().to(DEV).requires_grad_(True)
+    out = GATConvFunction.apply(xd, W, a_s, a_d, b, g, 0.2, p, seed)
+    (out * go.to(DEV)).sum().backward()
+    assert_close(out, ref, what="dropout forward, all classes")
+    assert_close_scaled(xd.grad, xr.grad, what="dropout grad_x")
+    assert_close_scaled(W.grad, conv.lin_src.weight.grad, what="dropout grad_W")
+    assert_close_scaled(a_s.grad, conv.att_src.grad.reshape(-1), what="dropout grad_att_src")
+    assert_close_scaled(a_d.grad, conv.att_dst.grad.reshape(-1), what="dropout grad_att_dst")
+    assert_close_scaled(b.grad, conv.bias.grad, what="dropout grad_bias")
+
+
 @pytest.mark.slow
 def test_full_size_sampled_parity_and_invariants():
     """C4-shaped graph (2M nodes / 10M edges here to bound test time): exact
