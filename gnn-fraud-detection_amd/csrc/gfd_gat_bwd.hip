@@ -28,6 +28,7 @@
 //   k_att_grad    grad_att from the S / T rows of grad_W'
 //   k_gemm        grad_x = dh W (only when requested)
 // Deterministic: no float atomics anywhere; every sum has a fixed order.
+#include "gfd_check.h"
 #include "gfd_fwd.h"
 
 using namespace gfd;
@@ -1381,6 +1382,10 @@ gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ld
                                             plan ? plan->num_chunks : 0,
                                             src_plan ? src_plan->num_chunks : 0))
     return GFD_ERR_WORKSPACE;
+  {
+    const gfd_status cs = check_graph(rowptr, col, N, N, plan, colptr, csc_dst, csc_eid, M, stream);
+    if (cs != GFD_OK) return cs;
+  }
   if (x_dtype == GFD_DTYPE_BF16)
     return bwd_impl<XBF16>(static_cast<const uint16_t*>(xv), N, F, ldx, rowptr, col, plan, colptr,
                     csc_dst, csc_eid, src_plan, M, W, att_src, att_dst, slope, dp, seed, st, stats,

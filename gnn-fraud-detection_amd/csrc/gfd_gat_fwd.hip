@@ -16,6 +16,7 @@
 #include <mutex>
 #include <utility>
 
+#include "gfd_check.h"
 #include "gfd_fwd.h"
 
 using namespace gfd;
@@ -190,6 +191,8 @@ gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t N, int F, in
   }
   if (num_dst == 0) return GFD_OK;
   const PackLayout L = pack_layout(F);
+  s = check_graph(rowptr, col, num_dst, N, plan, nullptr, nullptr, nullptr, 0, stream);
+  if (s != GFD_OK) return s;
   AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, num_dst, dst_offset, st,
             static_cast<const char*>(packed), bias, slope, dp, seed, p, stages, out, stats,
             nullptr, nullptr, xmax, e};
@@ -255,6 +258,8 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
   a.st = st;
   a.packed = static_cast<const char*>(packed);
   a.xmax = xmax;
+  s = check_graph(rowptr, col, N, N, plan, nullptr, nullptr, nullptr, 0, stream);
+  if (s != GFD_OK) return s;
   s = gfd_gat_pack_weights(weight, att_src, att_dst, F, heads, channels, packed, stream_);
   if (s != GFD_OK) return s;
   if (hipMemsetAsync(xmax, 0, sizeof(float), stream) != hipSuccess) return GFD_ERR_HIP;

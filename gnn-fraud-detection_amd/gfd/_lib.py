@@ -148,6 +148,18 @@ def load(path: str = LIB_PATH):
     return _LIB
 
 
+def open_variant(path: str):
+    """A separately built library of the same ABI (e.g. the bounds-checked
+    diagnostic build ``libgfd_checked.so``), with the signature table applied;
+    does not replace the process-wide library of ``load()``."""
+    lib = ct.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
 def call(name: str, *args):
     st = getattr(load(), name)(*args)
     if st != 0:

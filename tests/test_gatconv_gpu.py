@@ -364,3 +364,57 @@ def test_full_size_sampled_parity_and_invariants():
     Wbar = conv.lin_src.weight.view(8, 64, F).mean(0)
     ref_lone = x.cpu()[lone] @ Wbar.t() + conv.bias
     assert_close(out[lone.to(DEV)], ref_lone.detach(), what="self-loop-only rows")
+
+
+def test_checked_build_accepts_valid_graphs():
+    """The bounds-checked diagnostic build (-DGFD_CHECKED, libgfd_checked.so:
+    every index array validated on the device before the kernels run) gives
+    the product library's forward and backward on a valid graph with hubs and
+    every class (no false positives).  Skipped when the variant was not built."""
+    import os
+    from gfd import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libgfd_checked.so")
+    if not os.path.exists(path):
+        pytest.skip("libgfd_checked.so not built (GFD_BUILD_VARIANT=checked GFD_EXTRA_FLAGS=-DGFD_CHECKED)")
+    chk = _lib.open_variant(path)
+    prod = _lib.load()
+    _, graph = _gfd()
+    N, F = 6000, 166
+    x, ei, conv = _random_case(N, 48000, F, seed=31)
+    g = graph.get_graph(ei.to(DEV), N)
+    plan, csc = g.plan(), g.csc()
+    xd = x.to(DEV).contiguous()
+    W = conv.lin_src.weight.detach().to(DEV).contiguous()
+    a_s = conv.att_src.detach().to(DEV).reshape(-1).contiguous()
+    a_d = conv.att_dst.detach().to(DEV).reshape(-1).contiguous()
+    b = conv.bias.detach().to(DEV)
+    go = torch.randn(N, 64, device=DEV)
+    stream = _lib.stream_handle(DEV)
+    res = []
+    for lib in (prod, chk):
+        out = torch.empty(N, 64, device=DEV)
+        st = torch.empty(N, 16, device=DEV)
+        stats = torch.empty(N, 16, device=DEV)
+        ws = torch.empty(lib.gfd_gat_fwd_workspace_size(N, N, F, 8, 64, plan.num_hubs, plan.num_chunks),
+                         dtype=torch.uint8, device=DEV)
+        assert lib.gfd_gat_fwd(xd.data_ptr(), 0, N, F, F, g.rowptr.data_ptr(), g.col.data_ptr(),
+                               W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), b.data_ptr(), 8, 64,
+                               0.2, 0.0, 0, plan.cstruct(), out.data_ptr(), st.data_ptr(),
+                               stats.data_ptr(), ws.data_ptr(), ws.numel(), stream) == 0
+        gw = torch.empty_like(W)
+        ga, gd = torch.empty_like(a_s), torch.empty_like(a_d)
+        gb = torch.empty(64, device=DEV)
+        bws = torch.empty(lib.gfd_gat_bwd_workspace_size(N, g.num_messages, F, 8, 64, plan.num_hubs,
+                                                         plan.num_chunks, csc.plan.num_chunks),
+                          dtype=torch.uint8, device=DEV)
+        assert lib.gfd_gat_bwd(xd.data_ptr(), 0, N, F, F, g.rowptr.data_ptr(), g.col.data_ptr(),
+                               plan.cstruct(), csc.colptr.data_ptr(), csc.dst.data_ptr(),
+                               csc.eid.data_ptr(), csc.plan.cstruct(), g.num_messages, W.data_ptr(),
+                               a_s.data_ptr(), a_d.data_ptr(), 8, 64, 0.2, 0.0, 0, st.data_ptr(),
+                               stats.data_ptr(), go.data_ptr(), None, gw.data_ptr(), ga.data_ptr(),
+                               gd.data_ptr(), gb.data_ptr(), bws.data_ptr(), bws.numel(),
+                               stream) == 0
+        torch.cuda.synchronize()
+        res.append((out, gw, ga, gd, gb))
+    for u, v in zip(*res):
+        assert torch.equal(u, v)
