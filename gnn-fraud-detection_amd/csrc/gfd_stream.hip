@@ -57,12 +57,6 @@ constexpr int kSWaves = 8;
 #ifndef GFD_GENERAL_AP
 #define GFD_GENERAL_AP 1
 #endif
-// 1: the light class runs k_light_merged (projection of tile v and aggregation
-// of each wave's first slot of tile v + 1 in one phase; 2: both slots) when F
-// fills three feature chunks (F 129..168)
-#ifndef GFD_LIGHT_MERGED
-#define GFD_LIGHT_MERGED 0
-#endif
 // A-fragment k-steps read ahead in the MFMA loop (general; light fp32 / bf16
 // rows).  Light fp32: 1 keeps the kernel spill-free with 6 rows per slot in
 // flight (C4 light 6.73 -> 6.22 ms against 2); light bf16: 2 (C5 33.3 vs 33.7 ms)
@@ -581,300 +575,6 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   if (!kh) reduce_store(acc_prev, int((nv - 1) & 1));  // last tile
 }
 
-// ---------------------------------------------------------------------------
-// k_light_merged: the light class with the projection of tile v and the
-// aggregation of tile v + 1 in ONE phase.  k_stream runs them as two
-// barrier-separated phases, so both waves of a SIMD are in the MFMA phase
-// (VALU idle) or in the aggregation phase (matrix pipe idle) at the same time.
-// Here every wave interleaves its k-steps of MFMA(v) with the pieces of its
-// two slots' aggregation of tile v + 1 (softmax, one FMA block per message)
-// and keeps z in registers until the barrier after which Z(v + 1) may
-// overwrite Z(v); the rows those messages freed are re-issued for tile v + 2
-// after that barrier, with the Z writes:
-//   [MFMA(v) || aggregate(v + 1) -> z regs] -> barrier ->
-//   [z -> Z(v + 1) rows and row scales, issue tile v + 2] -> barrier
-// (re-issuing rows during the MFMA phase keeps 36 more VGPRs live than fit).
-// LDS ownership as in k_stream: ring parity t & 1 holds tile t's descriptors
-// (written when tile t's rows are issued, read when tile t is aggregated).
-template <typename XT, int KF, int KHM, int LO, bool EXACT>
-__global__ void __launch_bounds__(kSWaves * 64, 2) k_light_merged(
-    const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
-    int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
-    const int32_t* __restrict__ cols8, const float* __restrict__ st,
-    const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
-    const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
-    uint64_t seed, float* __restrict__ out, float* __restrict__ stats,
-    const float* __restrict__ xmax, const int64_t* __restrict__ split, int to_end, Epi ep) {
-  constexpr bool LIGHT = true;
-  constexpr int NL = kLightMax;
-  extern __shared__ __attribute__((aligned(16))) char ssm[];
-  const int ZS = 8 * Fp + 8;
-  const int KH = EXACT ? KHM : Fp / 8;
-  _Float16* Zh = reinterpret_cast<_Float16*>(ssm);
-  _Float16* Zl = Zh + kTile * ZS;
-  f32x4* red0 = reinterpret_cast<f32x4*>(Zl + kTile * ZS);
-  SlotRing* ring0 = reinterpret_cast<SlotRing*>(red0 + 2 * 4 * 64);
-  float* rsc0 = reinterpret_cast<float*>(ring0 + 2 * kTile);
-  int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);
-  uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);
-
-  const int wave = wave_uniform(threadIdx.x >> 6);
-  const int ct = wave & 3, kh = wave >> 2;
-  const int r0 = 2 * wave, r1 = r0 + 1;
-  const int64_t G = gridDim.x;
-  const int64_t t0 = blockIdx.x;
-  const int64_t tb = (split[0] + kTile - 1) / kTile;
-  const int64_t te = ((to_end ? num_dst : split[1]) + kTile - 1) / kTile;
-  const int64_t nv = t0 < te - tb ? (te - tb - 1 - t0) / G + 1 : 0;
-  const int64_t lim = to_end ? num_dst : split[1];
-  int lane = opaque(threadIdx.x & 63);
-  auto slot = [&](int64_t v, int r) { return (tb + t0 + v * G) * kTile + r; };
-
-  const float bcol = bias ? bias[ct * 16 + (lane & 15)] : 0.f;
-  const float wu = hdr->w_unscale;
-  const int erg = global_scale_exp(xmax, dp);
-  const float sg = erg != 127 ? ldexpf(1.0f, erg) : 1.0f;
-  constexpr int NR = KHM - LO;
-  f16x8 bh[KHM], bl[NR > 0 ? NR : 1];
-#pragma unroll
-  for (int u = 0; u < KHM; ++u) {
-    uint4 vh = make_uint4(0, 0, 0, 0), vl = vh;
-    if (u < KH) {
-      const int idx = ((kh * KH + u) * 4 + ct) * 64 + lane;
-      vh = wsh[idx];
-      vl = wsl[idx];
-    }
-    bh[u] = *reinterpret_cast<const f16x8*>(&vh);
-    if (u < NR) bl[u < NR ? u : 0] = *reinterpret_cast<const f16x8*>(&vl);
-    else WL[(wave * LO + (u - NR)) * 64 + lane] = vl;
-  }
-  if (nv == 0) return;  // block-uniform: no barrier below is reached by anyone
-
-  SlotRec n0, n1;
-  SlotRows<KF, NL> d0, d1;
-#define GFD_MI(P, n, d, rg) \
-  sl_issue_part<P, XT, KF, LIGHT>(n, d, x, ldx, F, col, st, dst_offset, rg, lane)
-  auto issue_all = [&](SlotRec& n, SlotRows<KF, NL>& d, SlotRing* rg) {
-    GFD_MI(0, n, d, rg); GFD_MI(1, n, d, rg); GFD_MI(2, n, d, rg); GFD_MI(3, n, d, rg);
-    GFD_MI(4, n, d, rg);
-    if constexpr (NL >= 5) GFD_MI((NL >= 5 ? 5 : 4), n, d, rg);
-    if constexpr (NL >= 6) GFD_MI((NL >= 6 ? 6 : 4), n, d, rg);
-    if constexpr (NL >= 7) GFD_MI((NL >= 7 ? 7 : 4), n, d, rg);
-  };
-#undef GFD_MI
-
-  // softmax of one light slot: p (message lane >> 3, head lane & 7; dropout
-  // applied; the global scale folded in when erg < 127) and 1 / (sum + eps)
-  auto softmax = [&](const int4 dd, const SlotRows<KF, NL>& q, float& p, float& inv) {
-    const int kk = lane >> 3;
-    const int n = dd.z - dd.y;
-    const float vv = leaky01(q.sj + q.th, slope);
-    const float m = max_xor8_16_32(kk < n ? vv : -INFINITY);
-    const float pe = kk < n ? __expf(vv - m) : 0.f;
-    const float l = sum_xor8_16_32(pe);
-    if (__builtin_expect(stats != nullptr, 0) && lane < 8 && dd.x >= 0) {
-      float* sr = stats + int64_t(dd.x) * 16 + lane;
-      sr[0] = m;
-      sr[8] = l;
-    }
-    inv = __builtin_amdgcn_rcpf(l + kSoftmaxEps);
-    float pd = pe;
-    if (__builtin_expect(dp > 0.f, 0))
-      pd = dropout_keep(seed, uint32_t(dd.y + kk), uint32_t(lane & 7), dp)
-               ? pe * (1.0f / (1.0f - dp)) : 0.f;
-    p = erg != 127 ? pd * (inv * sg) : pd;
-  };
-  // z += p_k x_k for message k of the slot (one FMA block, head pairs)
-  auto fma_msg = [&](f32x2 (&z)[4][KF], const SlotRows<KF, NL>& q, float p, int k) {
-    f32x2 p2[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) p2[g] = bcast2(p, 8 * k + 2 * g);
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int qq = 0; qq < KF; ++qq)
-        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{q.xv[k][qq], q.xv[k][qq]}, z[g][qq]);
-  };
-  // z -> fp16 hi / lo Z row + row scale (after the barrier that retires Z(v))
-  auto write_slot = [&](const int4 dd, const f32x2 (&z)[4][KF], float inv, int r, int tpar) {
-    float* rsc = rsc0 + tpar * kTile;
-    int* rid = rid0 + tpar * kTile;
-    if (dd.x < 0) {
-      if (lane == 0) rid[r] = -1;
-      return;
-    }
-    f16x8 hi[KF], lo[KF];
-    int er = erg;
-    if (erg != 127) split_zrow<KF>(z, hi, lo);
-    else er = pack_zrow<KF>(z, inv, erg, hi, lo);
-    write_zrow<KF>(hi, lo, Fp, lane, Zh + r * ZS, Zl + r * ZS);
-    if (lane == 0) {
-      rsc[r] = ldexpf(1.0f, -er);
-      rid[r] = dd.x;
-    }
-  };
-  auto reduce_store = [&](const f32x4& acc, int tpar) {
-    const float* rsc = rsc0 + tpar * kTile;
-    const int* rid = rid0 + tpar * kTile;
-    const f32x4 sum = acc + red0[(tpar * 4 + ct) * 64 + lane];
-    const int n = ct * 16 + (lane & 15);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = (lane >> 4) * 4 + q;
-      const int ri = rid[r];
-      if (ri >= 0) out[int64_t(ri) * C + n] = epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep);
-    }
-  };
-  auto zero_z = [&](f32x2 (&z)[4][KF]) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
-  };
-
-  f32x2 z0[4][KF], z1[4][KF];
-  float p0 = 0.f, p1 = 0.f, i0 = 1.f, i1 = 1.f;
-  int4 da = make_int4(-1, 0, 0, -1), db = da;
-  int kmax = 0;
-
-  // ---- prologue: tile 0 issued, aggregated and written; tile 1 issued ----
-  sl_rec(n0, slot(0, r0), num_dst, lim, desc, cols8, lane);
-  sl_rec(n1, slot(0, r1), num_dst, lim, desc, cols8, lane);
-  issue_all(n0, d0, ring0 + r0);
-  issue_all(n1, d1, ring0 + r1);
-  sl_rec(n0, slot(1, r0), num_dst, lim, desc, cols8, lane);
-  sl_rec(n1, slot(1, r1), num_dst, lim, desc, cols8, lane);
-  da = uni4(ring0[r0].d);
-  db = uni4(ring0[r1].d);
-  kmax = max(da.z - da.y, db.z - db.y);
-  zero_z(z0);
-  softmax(da, d0, p0, i0);
-#pragma unroll
-  for (int k = 0; k < NL; ++k)
-    if (k < kmax) fma_msg(z0, d0, p0, k);
-  write_slot(da, z0, i0, r0, 0);
-  if (nv > 1) issue_all(n0, d0, ring0 + kTile + r0);
-  zero_z(z1);
-  softmax(db, d1, p1, i1);
-#pragma unroll
-  for (int k = 0; k < NL; ++k)
-    if (k < kmax) fma_msg(z1, d1, p1, k);
-  write_slot(db, z1, i1, r1, 0);
-  if (nv > 1) issue_all(n1, d1, ring0 + kTile + r1);
-  sl_rec(n0, slot(2, r0), num_dst, lim, desc, cols8, lane);
-  sl_rec(n1, slot(2, r1), num_dst, lim, desc, cols8, lane);
-  __syncthreads();
-
-  f32x4 acc_prev = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t v = 0; v < nv; ++v) {
-    lane = opaque(threadIdx.x & 63);
-    const int par = int(v & 1);
-    const int pn = par ^ 1;
-    const bool more = v + 1 < nv;   // tile v + 1 exists: aggregate it
-    SlotRing* rgn = ring0 + pn * kTile;
-    const int aoff = (lane & 15) * ZS + 8 * (lane >> 4) + 32 * kh * KH;
-    const _Float16* ah = Zh + aoff;
-    const _Float16* al = Zl + aoff;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    if (more) {
-      da = uni4(rgn[r0].d);
-      db = uni4(rgn[r1].d);
-      kmax = max(da.z - da.y, db.z - db.y);
-    }
-    // aggregation pieces between the k-steps: k-step 1 softmax (slot 0),
-    // 2 .. 2 + NL - 1 its messages, then the same for slot 1
-    constexpr int PS1 = 2 + NL;
-#pragma unroll
-    for (int u = 0; u < KHM; ++u) {
-      if (u < KH) {
-        const f16x8 ahi = *reinterpret_cast<const f16x8*>(ah + 32 * u);
-        const f16x8 alo = *reinterpret_cast<const f16x8*>(al + 32 * u);
-        f16x8 blo;
-        if (u < NR) {
-          blo = bl[u < NR ? u : 0];
-        } else {
-          const uint4 w = WL[(wave * LO + (u - NR)) * 64 + lane];
-          blo = *reinterpret_cast<const f16x8*>(&w);
-        }
-        f32x4& acc = (u & 1) ? acc1 : acc0;
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[u], acc, 0, 0, 0);
-      }
-      if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
-      if (more) {
-        if (u == 1) {
-          softmax(da, d0, p0, i0);
-          zero_z(z0);
-        }
-#pragma unroll
-        for (int k = 0; k < NL; ++k)
-          if (u == 2 + k && k < kmax) fma_msg(z0, d0, p0, k);
-#if GFD_LIGHT_MERGED == 2
-        if (u == PS1) {  // z1 live from here: slot 0's rows are dead
-          softmax(db, d1, p1, i1);
-          zero_z(z1);
-        }
-#pragma unroll
-        for (int k = 0; k < NL; ++k)
-          if (u == PS1 + 1 + k && k < kmax) fma_msg(z1, d1, p1, k);
-#endif
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    acc0 += acc1;
-    if (kh) red0[(par * 4 + ct) * 64 + lane] = acc0;
-    acc_prev = acc0;
-    __syncthreads();  // partials visible; every Z read of tile v done
-    if (more) {
-      write_slot(da, z0, i0, r0, pn);
-      // tile v + 2: rows into the freed registers, its ring parity = par
-      if (v + 2 < nv) issue_all(n0, d0, ring0 + par * kTile + r0);
-#if GFD_LIGHT_MERGED != 2
-      // (GFD_LIGHT_MERGED 1: slot 1 aggregated here, after the barrier)
-      softmax(db, d1, p1, i1);
-      zero_z(z1);
-#pragma unroll
-      for (int k = 0; k < NL; ++k)
-        if (k < kmax) fma_msg(z1, d1, p1, k);
-#endif
-      write_slot(db, z1, i1, r1, pn);
-      if (v + 2 < nv) {
-        issue_all(n1, d1, ring0 + par * kTile + r1);
-        sl_rec(n0, slot(v + 3, r0), num_dst, lim, desc, cols8, lane);
-        sl_rec(n1, slot(v + 3, r1), num_dst, lim, desc, cols8, lane);
-      }
-    }
-    __syncthreads();  // Z of tile v + 1 complete
-  }
-  if (!kh) reduce_store(acc_prev, int((nv - 1) & 1));
-}
-
-template <typename XT, int KF, int KHM, int LO, bool EXACT>
-gfd_status launch_light_merged_k(const AggArgs& a, const PackLayout& L, bool to_end,
-                                 hipStream_t stream) {
-  auto kern = &k_light_merged<XT, KF, KHM, LO, EXACT>;
-  if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
-  const size_t lds = size_t(2) * 2 * kTile * (8 * L.Fp + 8) + sizeof(f32x4) * 2 * 4 * 64 +
-                     sizeof(SlotRing) * 2 * kTile + sizeof(float) * 4 * kTile +
-                     sizeof(uint4) * kSWaves * LO * 64;
-  if (L.KS / 2 > KHM || lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;
-  if (!ensure_lds(reinterpret_cast<const void*>(kern), lds)) return GFD_ERR_HIP;
-  const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
-  int64_t grid = cu_count();
-  if (grid > tiles) grid = tiles;
-  const gfd_plan& p = a.plan;
-  kern<<<int(grid), kSWaves * 64, lds, stream>>>(
-      a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
-      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
-      reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
-      reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
-      reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
-      a.out, a.stats, a.xmax, p.class_split, to_end ? 1 : 0, a.ep);
-  GFD_LAUNCH_CHECK();
-  return GFD_OK;
-}
-
 size_t stream_smem(int Fp, int lo) {
   return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 2 * 4 * 64 +
          sizeof(SlotRing) * 2 * kTile + sizeof(float) * 4 * kTile +
@@ -943,13 +643,6 @@ gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols || !p.class_split) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-#if GFD_LIGHT_MERGED
-  if (kf_for(a.F) == 3 && L.KS / 2 == 21) {
-    return a.xdt == GFD_DTYPE_BF16
-               ? launch_light_merged_k<XBF16, 3, 21, 8, true>(a, L, to_end, stream)
-               : launch_light_merged_k<XF32, 3, 21, 8, true>(a, L, to_end, stream);
-  }
-#endif
   return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, stream)
                                  : launch_stream_x<XF32, true>(a, L, to_end, stream);
 }

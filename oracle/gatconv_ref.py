@@ -196,6 +196,32 @@ class gatconv_forward_sampled:  # noqa: N801 (a namespace: prepare once, run man
                 "rows": nodes.numel(), "dsts": dsts.cpu()}
 
     @staticmethod
+    def prepare_indices(rowptr: torch.Tensor, col: torch.Tensor, dsts: torch.Tensor) -> dict:
+        """``prepare`` without copying rows: the index arrays only (host), so
+        ``run_from`` gathers the rows out of the full host feature matrix."""
+        dsts = dsts.long()
+        rp = rowptr.long()
+        starts, ends = rp[dsts], rp[dsts + 1]
+        lens = ends - starts
+        seg = torch.repeat_interleave(torch.arange(dsts.numel(), device=dsts.device), lens)
+        off = torch.cumsum(lens, 0) - lens
+        pos = starts[seg] + torch.arange(int(lens.sum()), device=dsts.device) - off[seg]
+        j = col[pos].long()
+        nodes, inv = torch.unique(torch.cat([j, dsts]), return_inverse=True)
+        return {"nodes": nodes.cpu(), "jl": inv[:j.numel()].cpu(), "il": inv[j.numel():].cpu(),
+                "seg": seg.cpu(), "n": dsts.numel(), "rows": nodes.numel(), "dsts": dsts.cpu()}
+
+    @staticmethod
+    def run_from(x_host: torch.Tensor, idx: dict, weight: torch.Tensor, att_src: torch.Tensor,
+                 att_dst: torch.Tensor, bias: Optional[torch.Tensor],
+                 heads: int = 8) -> torch.Tensor:
+        """``run`` with the row gather out of the full host x inside (the
+        dataflow's index_select of the source rows, cache behaviour included)."""
+        sub = dict(idx)
+        sub["x"] = x_host.index_select(0, idx["nodes"]).float()
+        return gatconv_forward_sampled.run(sub, weight, att_src, att_dst, bias, heads)
+
+    @staticmethod
     def run(sub: dict, weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor,
             bias: Optional[torch.Tensor], heads: int = 8) -> torch.Tensor:
         H = heads
