@@ -7,7 +7,8 @@
 // Destinations are scheduled by class (the plan's descending-degree slot order):
 //   hubs  (> threshold messages)   k_hub_partial / k_hub_fin   (gfd_hub.hip)
 //   general (hub rows, 7+ msgs)    k_stream<LIGHT = false>  8 waves, W stationary
-//   light (2..kLightMax = 6 msgs)  k_stream<LIGHT = true>   (gfd_stream.hip)
+//   light (2..kLightMax = 6 msgs)  k_stream<LIGHT = true>   (gfd_stream.hip;
+//                                  opt-in k_light_fs, gfd_light.hip)
 //   lone  (self loop only)         k_lone   out = mean_h W_h x_i  (gfd_lone.hip)
 //   F > 168 / no plan              k_fused  (gfd_fused.hip)
 #pragma once
@@ -485,6 +486,10 @@ gfd_status launch_hubs(const AggArgs& a, const PackLayout& L, hipStream_t stream
 // tile stages; GFD_ERR_UNSUPPORTED when the configuration is outside the kernel's set
 gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end, hipStream_t stream);
+// the light class at Fp = 168 with the two K halves in alternating wave groups
+// (gfd_light.hip; a measured-slower experiment, taken only under -DGFD_LIGHT_FS=1)
+bool light_fs_supported(const AggArgs& a, const PackLayout& L);
+gfd_status launch_light_fs(const AggArgs& a, const PackLayout& L, bool to_end, hipStream_t stream);
 gfd_status launch_lone(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_fused(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_logits(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
