@@ -36,23 +36,20 @@ def main():
         layer.step()
     torch.cuda.synchronize()
     rd(buf, 0)
-    fs = getattr(lib, "gfd_prof_fs_read", None)
-    if fs is not None:   # k_light_fs: per wave group
-        fs.argtypes = [ct.c_void_p, ct.c_int]
-        fb = (ct.c_ulonglong * 16)()
-        fs(fb, 1)
+    ld = getattr(lib, "gfd_prof_lds_read", None)
+    if ld is not None:   # k_light_lds
+        ld.argtypes = [ct.c_void_p, ct.c_int]
+        lb = (ct.c_ulonglong * 9)()
+        ld(lb, 1)
         for _ in range(steps):
             layer.step()
         torch.cuda.synchronize()
-        fs(fb, 0)
-        tiles = fb[4] / steps
-        print(f"k_light_fs: {tiles:.0f} tiles/step")
-        per = lambda x: x / steps / max(tiles, 1) / 4
-        for g in range(2):
-            v = [fb[8 * g + i] for i in range(8)]
-            print(f"   group {g}: cycles per tile per wave: MFMA phase {per(v[0]):.0f} "
-                  f"(heads {per(v[5]):.0f}, k-loop {per(v[6]):.0f}), barrier {per(v[1]):.0f}, "
-                  f"aggregation {per(v[2]):.0f}, barrier {per(v[3]):.0f}")
+        ld(lb, 0)
+        tiles = lb[8] / steps
+        tot = sum(lb[:8])
+        print(f"k_light_lds: {tiles:.0f} tiles/step, {tot / steps / max(tiles, 1) / 8:.0f} cycles per tile (per wave)")
+        for n, x in zip(("D issue", "M mfma", "B2a", "P+B2b", "W vmcnt", "S store", "A alpha", "B1"), lb[:8]):
+            print(f"   {n:10s} {x / steps / max(tiles, 1) / 8:7.0f} cycles  {100.0 * x / max(tot, 1):5.1f} %")
     names = ("MFMA + next-tile issue", "barrier 1", "aggregation", "barrier 2")
     for cls, k in (("general", 0), ("light", 1)):
         v = [buf[6 * k + i] for i in range(6)]
