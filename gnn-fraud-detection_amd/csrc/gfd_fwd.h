@@ -7,9 +7,7 @@
 // Destinations are scheduled by class (the plan's descending-degree slot order):
 //   hubs  (> threshold messages)   k_hub_partial / k_hub_fin   (gfd_hub.hip)
 //   general (hub rows, 7+ msgs)    k_stream<LIGHT = false>  8 waves, W stationary
-//   light (2..kLightMax = 6 msgs)  k_light_lds  LDS-gathered rows, K over the waves
-//                                  (gfd_light_lds.hip); k_stream<LIGHT = true>
-//                                  when rows are not 16-B aligned or max |x| > 2^20
+//   light (2..kLightMax = 6 msgs)  k_stream<LIGHT = true>   (gfd_stream.hip)
 //   lone  (self loop only)         k_lone   out = mean_h W_h x_i  (gfd_lone.hip)
 //   F > 168 / no plan              k_fused  (gfd_fused.hip)
 #pragma once
@@ -34,9 +32,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // ---------------------------------------------------------------------------
 // Packed weights (gfd_gat_pack_weights).
 struct PackLayout {
-  int F, Fp, Fu, KP, KS, KB, KQ;
+  int F, Fp, Fu, KP, KS, KB;
   size_t hdr_off, uv_off, whi_off, wlo_off, wsh_off, wsl_off, wbh_off, wbl_off, wph_off, wpl_off,
-      uph_off, upl_off, ush_off, usl_off, wqh_off, wql_off, bytes;
+      uph_off, upl_off, ush_off, usl_off, bytes;
 };
 
 inline PackLayout pack_layout(int F) {
@@ -47,7 +45,6 @@ inline PackLayout pack_layout(int F) {
   L.KP = H * L.Fp;
   L.KS = L.KP / 32;           // MFMA k-steps over all heads
   L.KB = (F + 31) / 32;       // k-steps of the head-mean matrix (k_lone)
-  L.KQ = (F + 3) / 4;         // k-steps of the head-pair fragments (k_light_lds)
   size_t o = 0;
   L.hdr_off = o; o = align_up(o + 64, 256);
   L.uv_off = o; o = align_up(o + sizeof(float) * 2 * H * L.Fu, 256);
@@ -72,12 +69,6 @@ inline PackLayout pack_layout(int F) {
   // .. +7, the bf16 logits pass's 16-B loads)
   L.ush_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
   L.usl_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KB) * 64, 256);
-  // head-pair fragments (k_light_lds): k-step s covers features 4 s .. 4 s + 3
-  // and all 8 heads; lane group g holds heads 2 g, 2 g + 1 of those 4
-  // features (K position 8 g + 2 u + e <-> feature 4 s + u, head 2 g + e), lo
-  // unscaled
-  L.wqh_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KQ) * 4 * 64, 256);
-  L.wql_off = o; o = align_up(o + sizeof(uint4) * size_t(L.KQ) * 4 * 64, 256);
   L.bytes = o;
   return L;
 }
@@ -484,8 +475,6 @@ struct AggArgs {
   float* part; float* zhub;
   const float* xmax;  // max |x| over all rows of x (nullable): one scale for every Z row
   Epi ep;             // output epilogue (ep.ab == NULL: none)
-  float* lalpha;      // k_light_alpha -> k_light_lds: softmax weights per light slot (nullable)
-  int32_t* tkmax;     // ... and each tile's largest message count
 };
 
 int cu_count();
@@ -496,12 +485,6 @@ gfd_status launch_hubs(const AggArgs& a, const PackLayout& L, hipStream_t stream
 // tile stages; GFD_ERR_UNSUPPORTED when the configuration is outside the kernel's set
 gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end, hipStream_t stream);
-// the light class with LDS-gathered rows and K sliced over the waves
-// (gfd_light_lds.hip): 16-B aligned rows, F <= 168, a max |x| bound
-bool light_lds_supported(const AggArgs& a, const PackLayout& L);
-size_t light_alpha_bytes(int64_t num_dst);  // workspace of k_light_alpha's weights
-size_t light_tkmax_bytes(int64_t num_dst);  // ... and per-tile message counts
-gfd_status launch_light_lds(const AggArgs& a, const PackLayout& L, bool to_end, hipStream_t stream);
 gfd_status launch_lone(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_fused(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_logits(const void* x, int xdt, int64_t rows, int F, int64_t ldx,

@@ -151,15 +151,6 @@ void hub_ws_layout(Carve* c, int64_t num_hubs, int64_t num_chunks, const PackLay
   *zhub = c->take<float>(size_t(num_hubs) * L.KP);
 }
 
-// the light class's softmax weights and per-tile message counts (k_light_lds;
-// left null when the workspace ends before them: k_stream runs the class)
-void light_ws_layout(Carve* c, int64_t num_dst, AggArgs* a) {
-  float* al = c->take<float>(light_alpha_bytes(num_dst) / sizeof(float));
-  int32_t* tk = c->take<int32_t>(light_tkmax_bytes(num_dst) / sizeof(int32_t));
-  a->lalpha = c->ok ? al : nullptr;
-  a->tkmax = c->ok ? tk : nullptr;
-}
-
 }  // namespace
 
 extern "C" {
@@ -167,6 +158,7 @@ extern "C" {
 size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int heads,
                                   int channels, int64_t num_hubs, int64_t num_chunks) {
   if (!check_hc(heads, channels, F)) return 0;
+  (void)num_dst;
   const PackLayout L = pack_layout(F);
   Sizer s;
   s.take<float>(size_t(num_chunks) * (16 + L.KP));    // hub partials
@@ -174,8 +166,6 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int
   s.take<char>(L.bytes);                              // packed weights (gfd_gat_fwd only)
   s.take<float>(size_t(num_nodes) * 16);              // st (gfd_gat_fwd when st == NULL)
   s.take<float>(1);                                   // max |x| (gfd_gat_fwd)
-  s.take<float>(light_alpha_bytes(num_dst) / sizeof(float));    // light softmax weights
-  s.take<int32_t>(light_tkmax_bytes(num_dst) / sizeof(int32_t));  // light tile counts
   return s.off;
 }
 
@@ -205,15 +195,10 @@ gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t N, int F, in
   if (s != GFD_OK) return s;
   AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, num_dst, dst_offset, st,
             static_cast<const char*>(packed), bias, slope, dp, seed, p, stages, out, stats,
-            nullptr, nullptr, xmax, e, nullptr, nullptr};
+            nullptr, nullptr, xmax, e};
   Carve c(ws, ws_bytes);
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.zhub);
   if (!c.ok && p.num_hubs > 0) return GFD_ERR_WORKSPACE;
-  // same order as gfd_gat_fwd_workspace_size: packed, st, max |x| (unused here)
-  (void)c.take<char>(L.bytes);
-  (void)c.take<float>(size_t(N) * 16);
-  (void)c.take<float>(1);
-  light_ws_layout(&c, num_dst, &a);
   return aggregate_impl(a, stream);
 }
 
@@ -263,12 +248,11 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
   const PackLayout L = pack_layout(F);
   Carve c(ws, ws_bytes);
   AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p,
-            GFD_STAGE_ALL, out, stats, nullptr, nullptr, nullptr, e, nullptr, nullptr};
+            GFD_STAGE_ALL, out, stats, nullptr, nullptr, nullptr, e};
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.zhub);
   void* packed = c.take<char>(L.bytes);
   float* st_ws = c.take<float>(size_t(N) * 16);
   float* xmax = c.take<float>(1);
-  light_ws_layout(&c, N, &a);
   if (!c.ok) return GFD_ERR_WORKSPACE;
   if (st == nullptr) st = st_ws;
   a.st = st;

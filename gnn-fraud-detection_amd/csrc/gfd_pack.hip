@@ -109,32 +109,6 @@ __global__ void k_pack_frag_s(const float* __restrict__ W, int F, int KS,
   wsl[idx] = lo.v;
 }
 
-// Head-pair fragments (k_light_lds): lane group g of k-step s holds heads
-// 2 g, 2 g + 1 of features 4 s .. 4 s + 3 (K position 8 g + 2 u + e <-> feature
-// 4 s + u, head 2 g + e), so a lane's A fragment is its destination's z for
-// one head pair and four consecutive features; lo = v - hi unscaled.
-__global__ void k_pack_frag_q(const float* __restrict__ W, int F, int KQ,
-                              const PackHeader* __restrict__ hdr, uint4* __restrict__ wqh,
-                              uint4* __restrict__ wql) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (s, ct, lane)
-  if (idx >= KQ * 4 * 64) return;
-  int lane = idx & 63, ct = (idx >> 6) & 3, s = idx >> 8;
-  int n = ct * 16 + (lane & 15);
-  int g = lane >> 4;
-  const float sc = hdr->w_scale * (1.0f / H);
-  union { uint4 v; _Float16 h[8]; } hi, lo;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int f = 4 * s + (j >> 1), h = 2 * g + (j & 1);
-    float v = (f < F) ? W[size_t(h * C + n) * F + f] * sc : 0.f;
-    _Float16 hv = (_Float16)v;
-    hi.h[j] = hv;
-    lo.h[j] = (_Float16)(v - (float)hv);
-  }
-  wqh[idx] = hi.v;
-  wql[idx] = lo.v;
-}
-
 // Head-mean fragments (k_lone): B[k = f][n] = mean_h W[h C + n][f] * 2^kb,
 // k-step s covers features 32 s .. 32 s + 31 (8 per lane group), lo unscaled.
 __global__ void k_pack_wbar(const float* __restrict__ W, int F, int KB,
@@ -419,11 +393,6 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   k_pack_frag_s<<<(n_fr + 255) / 256, 256, 0, stream>>>(weight, F, L.KS, hdr,
                                                         reinterpret_cast<uint4*>(p + L.wsh_off),
                                                         reinterpret_cast<uint4*>(p + L.wsl_off));
-  GFD_LAUNCH_CHECK();
-  const int n_fq = L.KQ * 4 * 64;
-  k_pack_frag_q<<<(n_fq + 255) / 256, 256, 0, stream>>>(weight, F, L.KQ, hdr,
-                                                        reinterpret_cast<uint4*>(p + L.wqh_off),
-                                                        reinterpret_cast<uint4*>(p + L.wql_off));
   GFD_LAUNCH_CHECK();
   const int n_wb = L.KB * 4 * 64;
   k_pack_wbar<<<(n_wb + 255) / 256, 256, 0, stream>>>(weight, F, L.KB, hdr,

@@ -350,11 +350,8 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
     uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
     float* __restrict__ stats, const float* __restrict__ xmax,
-    const int64_t* __restrict__ split, int to_end, Epi ep, int gate127) {
+    const int64_t* __restrict__ split, int to_end, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) char ssm[];
-  // gate127: launched beside k_light_lds, which takes the class unless the
-  // launch's Z scale is per row (erg = 127); then this kernel runs it
-  if (gate127 && global_scale_exp(xmax, dp) != 127) return;
   const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
   const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
   _Float16* Zh = reinterpret_cast<_Float16*>(ssm);              // [16][ZS]
@@ -585,7 +582,7 @@ size_t stream_smem(int Fp, int lo) {
 }
 
 template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
-gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end, bool gate127,
+gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
   auto kern = &k_stream<XT, KF, KHM, LO, EXACT, LIGHT>;
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
@@ -604,7 +601,7 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end, b
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,
-      a.zhub, a.out, a.stats, a.xmax, split, to_end ? 1 : 0, a.ep, gate127 ? 1 : 0);
+      a.zhub, a.out, a.stats, a.xmax, split, to_end ? 1 : 0, a.ep);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
@@ -613,17 +610,17 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end, b
 // for one / two / three feature chunks (F <= 64 / 128 / 168).  KF = 3 keeps
 // W_lo of 8 k-steps per wave in LDS.
 template <typename XT, bool LIGHT>
-gfd_status launch_stream_x(const AggArgs& a, const PackLayout& L, bool to_end, bool gate127,
+gfd_status launch_stream_x(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
   const int KF = kf_for(a.F);
   const bool exact = L.KS / 2 == (KF == 1 ? 8 : KF == 2 ? 16 : 21);
   switch (KF) {
-    case 1: return exact ? launch_stream_k<XT, 1, 8, 0, true, LIGHT>(a, L, to_end, gate127, stream)
-                         : launch_stream_k<XT, 1, 8, 0, false, LIGHT>(a, L, to_end, gate127, stream);
-    case 2: return exact ? launch_stream_k<XT, 2, 16, 0, true, LIGHT>(a, L, to_end, gate127, stream)
-                         : launch_stream_k<XT, 2, 16, 0, false, LIGHT>(a, L, to_end, gate127, stream);
-    case 3: return exact ? launch_stream_k<XT, 3, 21, 8, true, LIGHT>(a, L, to_end, gate127, stream)
-                         : launch_stream_k<XT, 3, 21, 8, false, LIGHT>(a, L, to_end, gate127, stream);
+    case 1: return exact ? launch_stream_k<XT, 1, 8, 0, true, LIGHT>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 1, 8, 0, false, LIGHT>(a, L, to_end, stream);
+    case 2: return exact ? launch_stream_k<XT, 2, 16, 0, true, LIGHT>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 2, 16, 0, false, LIGHT>(a, L, to_end, stream);
+    case 3: return exact ? launch_stream_k<XT, 3, 21, 8, true, LIGHT>(a, L, to_end, stream)
+                         : launch_stream_k<XT, 3, 21, 8, false, LIGHT>(a, L, to_end, stream);
     default: return GFD_ERR_UNSUPPORTED;
   }
 }
@@ -637,8 +634,8 @@ gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t str
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, false>(a, L, false, false, stream)
-                                 : launch_stream_x<XF32, false>(a, L, false, false, stream);
+  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, false>(a, L, false, stream)
+                                 : launch_stream_x<XF32, false>(a, L, false, stream);
 }
 
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
@@ -646,19 +643,8 @@ gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols || !p.class_split) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-  // k_light_lds (LDS-gathered rows, K sliced over the waves) when the rows
-  // are 16-B aligned; k_stream then runs only if the launch's Z scale turns
-  // out to be per row (a device-side max |x| past 2^20)
-#ifndef GFD_LIGHT_LDS  // opt-in experiment: -DGFD_LIGHT_LDS=1 (measured slower)
-#define GFD_LIGHT_LDS 0
-#endif
-  const bool lds = GFD_LIGHT_LDS && light_lds_supported(a, L);
-  if (lds) {
-    const gfd_status s = launch_light_lds(a, L, to_end, stream);
-    if (s != GFD_OK) return s;
-  }
-  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, lds, stream)
-                                 : launch_stream_x<XF32, true>(a, L, to_end, lds, stream);
+  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, stream)
+                                 : launch_stream_x<XF32, true>(a, L, to_end, stream);
 }
 
 }  // namespace fwd

@@ -36,20 +36,6 @@ def main():
         layer.step()
     torch.cuda.synchronize()
     rd(buf, 0)
-    ld = getattr(lib, "gfd_prof_lds_read", None)
-    if ld is not None:   # k_light_lds
-        ld.argtypes = [ct.c_void_p, ct.c_int]
-        lb = (ct.c_ulonglong * 9)()
-        ld(lb, 1)
-        for _ in range(steps):
-            layer.step()
-        torch.cuda.synchronize()
-        ld(lb, 0)
-        tiles = lb[8] / steps
-        tot = sum(lb[:8])
-        print(f"k_light_lds: {tiles:.0f} tiles/step, {tot / steps / max(tiles, 1) / 8:.0f} cycles per tile (per wave)")
-        for n, x in zip(("D issue", "M mfma", "B2a", "P+B2b", "W vmcnt", "S store", "A alpha", "B1"), lb[:8]):
-            print(f"   {n:10s} {x / steps / max(tiles, 1) / 8:7.0f} cycles  {100.0 * x / max(tot, 1):5.1f} %")
     names = ("MFMA + next-tile issue", "barrier 1", "aggregation", "barrier 2")
     for cls, k in (("general", 0), ("light", 1)):
         v = [buf[6 * k + i] for i in range(6)]

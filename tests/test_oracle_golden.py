@@ -95,7 +95,11 @@ def test_oracle_single_layer_vectors(golden, fixture, case):
     t = lambda k: torch.from_numpy(arr[f"{case}.{k}"])  # noqa: E731
     out = gatconv_forward(t("x"), t("edge_index"), t("weight"), t("att_src"), t("att_dst"),
                           t("bias"))
-    assert_close(out, arr[f"{case}.out"], atol=0, rtol=0, what=f"{fixture}/{case}")
+    # these fixtures are the oracle's own outputs (make_golden.py): a regression
+    # check of the restatement.  Not bit-exact across hosts: the CPU GEMM's
+    # reduction order depends on the ISA / thread count (1 ulp observed between
+    # an AVX-512 container and the one that wrote the fixtures).
+    assert_close(out, arr[f"{case}.out"], atol=1e-6, rtol=1e-6, what=f"{fixture}/{case}")
 
 
 def test_edgecase_fixture_covers_what_it_claims(golden):
