@@ -622,13 +622,31 @@ __device__ __forceinline__ void src_segment(const int32_t* __restrict__ csc_dst,
   }
 }
 
+// Per-column maxima of |dh'| (the grad_W' GEMM's A operand) and |x| (its B
+// operand) and each dh' row's power-of-two exponent (grad_x's A operand): the
+// fp16 3-term GEMMs scale every column (row) on its own, so a heavy-tailed
+// feature or gradient column does not push the others into fp16 subnormals.
+// amax[m] (m < kDH): dh' column m; amax[kDH + f]: x column f, as float bits
+// (non-negative floats order like their bits: an integer max is exact and
+// order-independent).  kAmaxCols = kDH + 256 words.
+constexpr int kAmaxCols = kDH + 256;
+
+__device__ __forceinline__ void amax_put(uint32_t* __restrict__ amax, int c, float v) {
+  const uint32_t bits = __float_as_uint(v);
+  // an atomic only when it beats the value already there (same-address
+  // atomics from every block otherwise serialise in L2)
+  if (bits > __atomic_load_n(amax + c, __ATOMIC_RELAXED)) atomicMax(amax + c, bits);
+}
+
 // dh' row j from y (lane = channel), ds (head lane & 7, complete) and dt_j;
-// returns the largest |value| the lane wrote (the grad_W' GEMM's scale)
+// folds |value| into the lane's per-column maxima (cm[hh]: column hh C +
+// lane; ct[0 / 1]: columns HC + lane / HC + H + lane, lanes < 8) and returns
+// the row's max |value| (every lane).
 __device__ __forceinline__ float write_dh(int64_t j, const float (&y)[H], float ds,
                                           const float* __restrict__ dt,
                                           const float* __restrict__ att_src,
                                           const float* __restrict__ att_dst,
-                                          float* __restrict__ dh) {
+                                          float* __restrict__ dh, float (&cm)[H], float (&ct)[2]) {
   const int lane = threadIdx.x & 63;
   float* r = dh + j * kDH;
   const float dtl = dt[j * 8 + (lane & 7)];
@@ -641,35 +659,40 @@ __device__ __forceinline__ float write_dh(int64_t j, const float (&y)[H], float 
                          fmaf(dsh, att_src[hh * C + lane], y[hh] * (1.0f / H)));
     r[hh * C + lane] = v;
     mx = fmaxf(mx, fabsf(v));
+    cm[hh] = fmaxf(cm[hh], fabsf(v));
   }
   if (lane < 8) {
     r[HC + lane] = ds;
     r[HC + H + lane] = dtl;
     mx = fmaxf(mx, fmaxf(fabsf(ds), fabsf(dtl)));
+    ct[0] = fmaxf(ct[0], fabsf(ds));
+    ct[1] = fmaxf(ct[1], fabsf(dtl));
   }
-  return mx;
+  return max_wave(mx);
 }
 
-// amax[0] = max |dh'|, amax[1] = max |x| as float bits (non-negative floats
-// order like their bits; an integer max is exact and order-independent).
-// Block maximum first, and an atomic only when it beats the value already
-// there (thousands of same-address atomics otherwise serialise in L2).
-__device__ __forceinline__ void amax_commit(float dm, float xm, uint32_t* __restrict__ amax) {
-  __shared__ float red[2][16];
-  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  dm = max_wave(dm);
-  xm = max_wave(xm);
-  if ((threadIdx.x & 63) == 0) {
-    red[0][w] = dm;
-    red[1][w] = xm;
+// Block-level per-column maxima (the block's waves' in LDS), then one
+// conditional atomic per column.  cm / ct as write_dh, xm[q]: x column
+// lane + 64 q (q < 4, F <= 256).
+__device__ __forceinline__ void amax_commit(const float (&cm)[H], const float (&ct)[2],
+                                            const float (&xm)[4], int F,
+                                            uint32_t* __restrict__ amax) {
+  __shared__ float red[4][kAmaxCols];  // 256-thread blocks
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) red[w][hh * C + lane] = cm[hh];
+  if (lane < 8) {
+    red[w][HC + lane] = ct[0];
+    red[w][HC + H + lane] = ct[1];
   }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[w][kDH + lane + 64 * q] = xm[q];
   __syncthreads();
-  if (threadIdx.x < 2) {
+  for (int c = threadIdx.x; c < kDH + F; c += blockDim.x) {
     float m = 0.f;
-    for (int k = 0; k < nw; ++k) m = fmaxf(m, red[threadIdx.x][k]);
-    const uint32_t bits = __float_as_uint(m);
-    if (bits > __atomic_load_n(amax + threadIdx.x, __ATOMIC_RELAXED))
-      atomicMax(amax + threadIdx.x, bits);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m = fmaxf(m, red[k][c]);
+    amax_put(amax, c, m);
   }
 }
 
@@ -680,22 +703,29 @@ __global__ void __launch_bounds__(256) k_bwd_src(
     const float* __restrict__ alpha_d, const float* __restrict__ dpre,
     const float* __restrict__ dt, const float* __restrict__ g, const float* __restrict__ att_src,
     const float* __restrict__ att_dst, const typename XT::T* __restrict__ x, int F, int64_t ldx,
-    float* __restrict__ dh, uint32_t* __restrict__ amax) {
+    float* __restrict__ dh, uint32_t* __restrict__ amax, int32_t* __restrict__ erow) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  float dm = 0.f, xm = 0.f;
+  float cm[H], ct[2] = {0.f, 0.f}, xm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) cm[hh] = 0.f;
   for (int64_t j = w0; j < N; j += nw) {
-    for (int f = lane; f < F; f += 64) xm = fmaxf(xm, fabsf(ldx1(x + j * ldx + f)));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = lane + 64 * q;
+      if (f < F) xm[q] = fmaxf(xm[q], fabsf(ldx1(x + j * ldx + f)));
+    }
     if (src_hub_rank && src_hub_rank[j] >= 0) continue;  // k_bwd_src_hub
     float y[H];
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) y[hh] = 0.f;
     float ds = 0.f;
     src_segment(csc_dst, csc_eid, colptr[j], colptr[j + 1], alpha_d, dpre, g, y, ds);
-    dm = fmaxf(dm, write_dh(j, y, sum_xor8_16_32(ds), dt, att_src, att_dst, dh));
+    const float rm = write_dh(j, y, sum_xor8_16_32(ds), dt, att_src, att_dst, dh, cm, ct);
+    if (lane == 0) erow[j] = scale_exp(rm);
   }
-  amax_commit(dm, xm, amax);
+  amax_commit(cm, ct, xm, F, amax);
 }
 
 // source hub chunks {hub, p0, p1, src}: partial y (512) | ds (8) per chunk
@@ -725,7 +755,7 @@ __global__ void __launch_bounds__(512) k_bwd_src_hub2(
     const float* __restrict__ spart, const int32_t* __restrict__ chunk_ptr,
     const int32_t* __restrict__ hub_src, const float* __restrict__ dt,
     const float* __restrict__ att_src, const float* __restrict__ att_dst,
-    float* __restrict__ dh, uint32_t* __restrict__ amax) {
+    float* __restrict__ dh, uint32_t* __restrict__ amax, int32_t* __restrict__ erow) {
   const int lane = threadIdx.x & 63, hh = threadIdx.x >> 6;
   const int64_t hb = blockIdx.x;
   const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
@@ -744,14 +774,26 @@ __global__ void __launch_bounds__(512) k_bwd_src_hub2(
   const float v = fmaf(dth, att_dst[hh * C + lane],
                        fmaf(sds[hh], att_src[hh * C + lane], y * (1.0f / H)));
   r[hh * C + lane] = v;
+  amax_put(amax, hh * C + lane, fabsf(v));  // one column per thread
   float mx = fabsf(v);
   if (hh == 0 && lane < 8) {
     const float dtl = dt[j * 8 + lane];
     r[HC + lane] = sds[lane];
     r[HC + H + lane] = dtl;
+    amax_put(amax, HC + lane, fabsf(sds[lane]));
+    amax_put(amax, HC + H + lane, fabsf(dtl));
     mx = fmaxf(mx, fmaxf(fabsf(sds[lane]), fabsf(dtl)));
   }
-  amax_commit(mx, 0.f, amax);
+  __shared__ float rmx[8];  // the row's max over the 8 waves
+  mx = max_wave(mx);
+  if (lane == 0) rmx[hh] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, rmx[k]);
+    erow[j] = scale_exp(m);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -807,6 +849,8 @@ __global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
                                             const uint32_t* __restrict__ amax,
                                             float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
+  // per-column power-of-two scales: dh' columns of this m-block, x columns
+  __shared__ float csa[kGM], csb[kGMaxF];
   const int b = blockIdx.x, rem = b % 24;
   const int mb = rem >> 3, s = (b / 24) * 8 + (rem & 7);
   if (s >= S) return;  // block-uniform, before any barrier
@@ -814,9 +858,10 @@ __global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
   const int NTn = Fu >> 4, nB = 16 * (Fu >> 2);  // B items: 16 node pairs x Fu / 4 chunks
-  const int ea = scale_exp(__uint_as_float(amax[0])), eb = scale_exp(__uint_as_float(amax[1]));
-  const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
-  const float ua = ldexpf(1.0f, -ea), ub = ldexpf(1.0f, -eb);  // two steps: 2^-(ea+eb) may underflow
+  if (tid < kGM) csa[tid] = ldexpf(1.0f, scale_exp(__uint_as_float(amax[mb * kGM + tid])));
+  if (tid < kGMaxF)
+    csb[tid] = tid < F ? ldexpf(1.0f, scale_exp(__uint_as_float(amax[kDH + tid]))) : 1.0f;
+  __syncthreads();
   _Float16* buf = reinterpret_cast<_Float16*>(gsm);
   const int bsz = 2 * (kGM + Fu) * kGPt;  // halves per buffer: A hi, A lo, B hi, B lo
   auto Ahi = [&](int u) { return buf + u * bsz; };
@@ -853,6 +898,7 @@ __global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           uint32_t lo;
+          const float sa = csa[4 * c + q];
           const uint32_t hi = pk_hi_lo(st.a[it][0][q] * sa, st.a[it][1][q] * sa, lo);
           ah[((4 * c + q) * kGPt >> 1) + p] = hi;
           al[((4 * c + q) * kGPt >> 1) + p] = lo;
@@ -862,6 +908,7 @@ __global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           uint32_t lo;
+          const float sb = csb[4 * c + q];
           const uint32_t hi = pk_hi_lo(st.b[it][0][q] * sb, st.b[it][1][q] * sb, lo);
           bh[((4 * c + q) * kGPt >> 1) + p] = hi;
           bl[((4 * c + q) * kGPt >> 1) + p] = lo;
@@ -932,10 +979,13 @@ __global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
       const int nt = wn + 2 * j;
       const int n = nt * 16 + (lane & 15);
       if (nt >= NTn || n >= F) continue;
+      const float ub = 1.0f / csb[n];  // exact: a power of two
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int m = mb * kGM + mt * 16 + 4 * (lane >> 4) + q;
-        Cz[int64_t(m) * F + n] = (acc[i][j][q] * ua) * ub;
+        const int ml = mt * 16 + 4 * (lane >> 4) + q;
+        const int m = mb * kGM + ml;
+        // two steps: 2^-(ea + eb) may underflow
+        Cz[int64_t(m) * F + n] = (acc[i][j][q] * (1.0f / csa[ml])) * ub;
       }
     }
   }
@@ -954,7 +1004,7 @@ __global__ void __launch_bounds__(512) k_gx(const float* __restrict__ dh, int64_
                                             const uint4* __restrict__ bhi,
                                             const uint4* __restrict__ blo,
                                             const float* __restrict__ whdr,
-                                            const uint32_t* __restrict__ amax,
+                                            const int32_t* __restrict__ erow,
                                             float* __restrict__ gx) {
   __shared__ uint4 Bh[kGxKS][kGxNT][64], Bl[kGxKS][kGxNT][64];
   const int NT = (F + 15) / 16;
@@ -967,15 +1017,15 @@ __global__ void __launch_bounds__(512) k_gx(const float* __restrict__ dh, int64_
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int ea = scale_exp(__uint_as_float(amax[0]));
-  const float sa = ldexpf(1.0f, ea);
-  const float un = ldexpf(1.0f, -ea) * whdr[0];
+  const float wun = whdr[0];
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwave = (int64_t(gridDim.x) * blockDim.x) >> 6;
   const int64_t tiles = (N + 15) / 16;
   for (int64_t t = wave; t < tiles; t += nwave) {
     const int64_t row = t * 16 + r;
-    const float* ar = dh + (row < N ? row : N - 1) * kDH + 8 * g;
+    const int64_t rc = row < N ? row : N - 1;
+    const float* ar = dh + rc * kDH + 8 * g;
+    const float sa = ldexpf(1.0f, erow[rc]);  // this row's own power-of-two scale
     f32x4 am[kGxNT], ax[kGxNT];
 #pragma unroll
     for (int ct = 0; ct < kGxNT; ++ct) am[ct] = ax[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1013,7 +1063,8 @@ __global__ void __launch_bounds__(512) k_gx(const float* __restrict__ dh, int64_
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t orow = t * 16 + 4 * g + q;
-        if (orow < N) gx[orow * F + n] = (am[ct][q] + ax[ct][q] * (1.0f / kLoScale)) * un;
+        if (orow < N)
+          gx[orow * F + n] = ((am[ct][q] + ax[ct][q] * (1.0f / kLoScale)) * ldexpf(1.0f, -erow[orow])) * wun;
       }
     }
   }
@@ -1150,7 +1201,7 @@ int gw_slabs(int64_t N) {
 int kf_fu(int F) { return (F + 63) / 64; }
 
 struct BwdLayout {
-  size_t whdr, amax, bhi, blo, dpre, alpha, dt, uhub, cpart, hadot, spart, dh, slab, gw, gbp;
+  size_t whdr, amax, erow, bhi, blo, dpre, alpha, dt, uhub, cpart, hadot, spart, dh, slab, gw, gbp;
 };
 
 BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
@@ -1161,7 +1212,8 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
   const int64_t ch = chunks > 0 ? chunks : 0;
   auto take = [&](size_t bytes) { size_t o = align_up(s.off, 256); s.off = o + bytes; return o; };
   L.whdr = take(64);
-  L.amax = take(64);
+  L.amax = take(sizeof(uint32_t) * kAmaxCols);
+  L.erow = take(sizeof(int32_t) * size_t(N));
   L.bhi = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
   L.blo = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
   L.dpre = take(sizeof(float) * size_t(M) * 8);
@@ -1250,6 +1302,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   char* b = static_cast<char*>(ws);
   float* whdr = reinterpret_cast<float*>(b + L.whdr);
   uint32_t* amax = reinterpret_cast<uint32_t*>(b + L.amax);
+  int32_t* erow = reinterpret_cast<int32_t*>(b + L.erow);
   uint4* bhi = reinterpret_cast<uint4*>(b + L.bhi);
   uint4* blo = reinterpret_cast<uint4*>(b + L.blo);
   float* dpre = reinterpret_cast<float*>(b + L.dpre);
@@ -1280,10 +1333,10 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   {
     int64_t blocks = (N + 3) / 4;
     if (blocks > 16384) blocks = 16384;
-    GFD_HIP_CHECK(hipMemsetAsync(amax, 0, 2 * sizeof(uint32_t), stream));
+    GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
     k_bwd_src<XT><<<unsigned(blocks), 256, 0, stream>>>(
         colptr, csc_dst, csc_eid, N, shubs > 0 ? src_plan->hub_rank : nullptr, alpha_d, dpre, dt,
-        g, att_src, att_dst, x, F, ldx, dh, amax);
+        g, att_src, att_dst, x, F, ldx, dh, amax, erow);
     GFD_LAUNCH_CHECK();
     if (shubs > 0) {
       k_bwd_src_hub1<<<unsigned((schunks + 3) / 4), 256, 0, stream>>>(
@@ -1292,7 +1345,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
       GFD_LAUNCH_CHECK();
       k_bwd_src_hub2<<<unsigned(shubs), 512, 0, stream>>>(spart, src_plan->hub_chunk_ptr,
                                                           src_plan->hub_dst, dt, att_src, att_dst,
-                                                          dh, amax);
+                                                          dh, amax, erow);
       GFD_LAUNCH_CHECK();
     }
   }
@@ -1330,7 +1383,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   if (grad_x && F <= 16 * kGxNT) {
     int64_t nb = ((N + 15) / 16 + 7) / 8;
     if (nb > cu_count()) nb = cu_count();
-    k_gx<<<unsigned(nb), 512, 0, stream>>>(dh, N, F, bhi, blo, whdr, amax, grad_x);
+    k_gx<<<unsigned(nb), 512, 0, stream>>>(dh, N, F, bhi, blo, whdr, erow, grad_x);
     GFD_LAUNCH_CHECK();
   } else if (grad_x) {
     dim3 grid(unsigned((N + GB - 1) / GB), unsigned((F + GB - 1) / GB));

@@ -167,6 +167,58 @@ def test_backward_bf16_features():
                           rtol=2 ** -7, atol=1e-3 * xr.grad.abs().max().item())
 
 
+def _per_column_close(got, ref, rtol, what, dim=0):
+    """|got - ref| <= rtol * (max |ref| along dim) per column (dim=0) or per row
+    (dim=1): a heavy-tailed column must not cost the other columns precision,
+    which a whole-tensor scale would hide."""
+    got = got.detach().cpu().double()
+    ref = ref.detach().cpu().double()
+    scale = ref.abs().amax(dim=dim, keepdim=True).clamp_min(1e-30)
+    rel = ((got - ref).abs() / scale).amax()
+    assert rel <= rtol, f"{what}: worst per-{'column' if dim == 0 else 'row'} error {rel:.3e} > {rtol}"
+
+
+@pytest.mark.parametrize("big", [1e6, 1e9])
+def test_backward_heavy_tailed_features(big):
+    """An outlier feature column: the grad_W' GEMM scales each x
+    and dh' column on its own, so the other columns keep fp32-faithful
+    products (one scale from max |x| pushed them into fp16 subnormals at 1e9).
+    The outlier feature has zero weight, so the attention (and dh') stay
+    well-conditioned and the fp32 oracle is a fair reference; every grad_W
+    column is checked against its own scale."""
+    gnn, _ = _gfd()
+    x, ei, conv = _random_case(3000, 24000, 166, seed=31)
+    x[:40, 0] = big * torch.linspace(-1, 1, 40)
+    with torch.no_grad():
+        conv.lin_src.weight[:, 0] = 0.0
+    g = torch.randn(3000, 64, generator=torch.Generator().manual_seed(7))
+    xr = x.clone().requires_grad_(True)
+    (conv(xr, ei) * g).sum().backward()
+    gx, gW, gas, gad, gb = _grads(gnn, x, ei, conv, g)
+    Wref = conv.lin_src.weight.grad  # [512, F]: columns = features
+    _per_column_close(gW, Wref, 2e-4, f"grad_W, outlier column {big:g}")
+    assert_close_scaled(gas, conv.att_src.grad, what="grad_att_src")
+    assert_close_scaled(gad, conv.att_dst.grad, what="grad_att_dst")
+    assert_close_scaled(gb, conv.bias.grad, what="grad_bias")
+
+
+def test_backward_heavy_tailed_gradient_rows():
+    """A destination whose upstream gradient is 10^6 times the others (hidden
+    layer, F = 64: grad_x on the fp16 MFMA path): each dh' row is scaled on its
+    own, so every row of grad_x keeps its precision."""
+    gnn, _ = _gfd()
+    x, ei, conv = _random_case(4000, 32000, 64, seed=32)
+    g = torch.randn(4000, 64, generator=torch.Generator().manual_seed(8))
+    g[5] *= 1e6
+    g[77] *= 1e-4
+    xr = x.clone().requires_grad_(True)
+    (conv(xr, ei) * g).sum().backward()
+    gx, gW, gas, gad, gb = _grads(gnn, x, ei, conv, g)
+    nz = xr.grad.abs().amax(dim=1) > 0
+    _per_column_close(gx[nz], xr.grad[nz], 2e-4, "grad_x per row", dim=1)
+    _per_column_close(gW, conv.lin_src.weight.grad, 2e-4, "grad_W per column")
+
+
 @pytest.mark.parametrize("threshold,chunk", [(1, 1), (4, 3), (16, 16), (1 << 30, 128)])
 @pytest.mark.parametrize("classes", [False, True])
 def test_hub_split_equivalence(threshold, chunk, classes):
