@@ -122,13 +122,16 @@ class Layer:
         self.packed = torch.empty(self.lib.gfd_gat_packed_size(F, H, C), dtype=torch.uint8,
                                   device=dev)
         self.st = torch.empty((self.N, 2 * H), dtype=torch.float32, device=dev)
-        rows = spec.node_hi - spec.node_lo
-        self.st_local = torch.empty((max(rows, 1), 2 * H), dtype=torch.float32, device=dev)
-        # N > 1: the source-logit half of every node block is all-gathered
-        # (gfd.dist.exchange_logits: [N, 8] instead of [N, 16])
-        per = (self.N + world - 1) // world
-        self.s_local = torch.zeros((per, H), dtype=torch.float32, device=dev)
-        self.s_all = torch.empty((per * world, H), dtype=torch.float32, device=dev)
+        # sharded (N > 1, or the tests' virtual shards): one fused logits + lone
+        # pass over the rank's own destinations; at N > 1 their source half is
+        # all-gathered-v (gfd.dist.exchange_logits: [N, 8] instead of [N, 16])
+        sizes = [spec.dst_bounds[r + 1] - spec.dst_bounds[r] for r in range(world)]
+        self.per = max(max(sizes), 1)
+        self.sizes = sizes
+        self.st_local = torch.empty((max(self.per, self.n_dst, 1), 2 * H), dtype=torch.float32,
+                                    device=dev)
+        self.s_local = torch.zeros((self.per, H), dtype=torch.float32, device=dev)
+        self.s_all = torch.empty((self.per * world, H), dtype=torch.float32, device=dev)
         self.out = torch.empty((max(self.n_dst, 1), C), dtype=torch.float32, device=dev)
         self.ws = torch.empty(self.lib.gfd_gat_fwd_workspace_size(
             self.N, self.n_dst, F, H, C, self.plan.num_hubs, self.plan.num_chunks),
@@ -136,10 +139,11 @@ class Layer:
         self.xmax = torch.zeros(1, dtype=torch.float32, device=dev)
         self.stream = _lib.stream_handle(dev)
         self.cplan = self.plan.cstruct()
-        # one shard = the whole graph: the lone destinations' outputs come out of
-        # the logits pass (gfd_gat_logits_lone) and the tile stage skips that class
-        self.fused = spec.dst_lo == 0 and spec.dst_hi == self.N and world == 1
-        self.stages = self.STAGES_FUSED if self.fused else self.STAGES
+        # the lone destinations' outputs come out of the logits pass
+        # (gfd_gat_logits_lone over the rank's destinations) and the tile stage
+        # skips that class -- whole graph or shard, at every world size
+        self.whole = spec.dst_lo == 0 and spec.dst_hi == self.N and world == 1
+        self.stages = self.STAGES_FUSED
 
     def pack_and_logits(self):
         s, _lib, F = self.s, self._lib, self.s["F"]
@@ -147,32 +151,36 @@ class Layer:
                   s["a_d"].data_ptr(), F, H, C, self.packed.data_ptr(), self.stream)
         self.xmax.zero_()
         x, spec = s["x"], s["spec"]
-        if self.fused:
+        if self.whole:
             _lib.call("gfd_gat_logits_lone", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
                       self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
                       s["bias"].data_ptr(), 0.2, self.st.data_ptr(), self.xmax.data_ptr(),
                       self.out.data_ptr(), None, self.stream)
-        elif self.world == 1:
+            return
+        # a shard: [s | t] and the lone outputs of the own destinations in one
+        # pass; the other rows' s from the all-gather (N > 1) or, for the tests'
+        # virtual shards on one GPU, from a logits pass over every row
+        n = self.n_dst
+        if self.world == 1:
             _lib.call("gfd_gat_logits_ex", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
                       self.packed.data_ptr(), H, C, self.st.data_ptr(), self.xmax.data_ptr(),
                       self.stream)
-        else:
-            # gfd.dist.exchange_logits with persistent buffers: s of the node
-            # block all-gathered, [s | t] of the own destinations computed here
+        if n > 0:
+            _lib.call("gfd_gat_logits_lone", x[spec.dst_lo:].data_ptr(), self.xdt, n, F,
+                      s["ldx"], self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
+                      s["bias"].data_ptr(), 0.2, self.st_local.data_ptr(), self.xmax.data_ptr(),
+                      self.out.data_ptr(), None, self.stream)
+        if self.world > 1:
             import torch.distributed as dist
-            rows = spec.node_hi - spec.node_lo
-            if rows > 0:
-                _lib.call("gfd_gat_logits_ex", x[spec.node_lo:].data_ptr(), self.xdt, rows, F,
-                          s["ldx"], self.packed.data_ptr(), H, C, self.st_local.data_ptr(),
-                          self.xmax.data_ptr(), self.stream)
-                self.s_local[:rows] = self.st_local[:rows, :H]
+            if n > 0:
+                self.s_local[:n] = self.st_local[:n, :H]
             dist.all_gather_into_tensor(self.s_all, self.s_local)
-            self.st[:, :H] = self.s_all[:self.N]
-            if self.n_dst > 0:
-                _lib.call("gfd_gat_logits_ex", x[spec.dst_lo:].data_ptr(), self.xdt, self.n_dst,
-                          F, s["ldx"], self.packed.data_ptr(), H, C,
-                          self.st[spec.dst_lo:].data_ptr(), self.xmax.data_ptr(), self.stream)
+            for r in range(self.world):
+                lo, sz = spec.dst_bounds[r], self.sizes[r]
+                self.st[lo:lo + sz, :H] = self.s_all[r * self.per:r * self.per + sz]
             dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
+        if n > 0:
+            self.st[spec.dst_lo:spec.dst_hi] = self.st_local[:n]
 
     def aggregate(self, stages):
         s = self.s
@@ -387,6 +395,9 @@ def measure(args, dev, rank, world, config):
         "roofline": {"bound": "hbm", "achieved": kernels[dom]["gbps"], "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": kernels[dom]["frac"],
                      "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                     # provenance of traffic: the git tree its PMC passes ran on
+                     "traffic_source": ({"tree": pmc.get("tree"), "source": pmc.get("source")}
+                                        if pmc else None),
                      "kernel": kname[dom], "algorithmic_bytes": sb[dom],
                      "kernel_ms": kernels[dom]["ms"]},
         "kernels": kernels,

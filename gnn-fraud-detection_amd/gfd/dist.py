@@ -9,10 +9,9 @@ balanced by message count (prefix sum over in-degree).
 Layer 0 keeps ``x`` halo-resident (every rank holds the rows its in-edges
 reference; for a power-law graph that is nearly all of x).  Only the SOURCE
 logits s_j cross GPUs (``exchange_logits``): each rank computes ``[s | t]`` for
-an equal node block, all-gathers the s half (``[N, H]`` fp32: 32 B per node
-instead of the 664 B feature row -- the "halo" of the north star), and
-recomputes ``[s | t]`` for its own destination block, whose t it is the only
-reader of.  The fused aggregate-project kernels then run on the local shard
+its own destination block (whose t it is the only reader of) and all-gathers
+the s half (``[N, H]`` fp32: 32 B per node instead of the 664 B feature row --
+the "halo" of the north star).  The fused aggregate-project kernels then run on the local shard
 with no further communication.  Hidden layers all-gather the previous layer's
 ``[N, 64]`` output instead.
 """
@@ -66,8 +65,9 @@ class ShardSpec:
     """One rank's share of a destination-sharded layer.
 
     ``dst_lo:dst_hi`` -- the destinations (and so the CSR messages) this rank
-    owns, balanced by message count; ``node_lo:node_hi`` -- the equal node
-    block whose attention logits this rank computes before the all-gather.
+    owns, balanced by message count; their attention logits are this rank's
+    share of the exchange.  ``node_lo:node_hi`` -- an equal node block (the
+    tests' per-rank logits blocks).
     """
 
     def __init__(self, rowptr: torch.Tensor, rank: int, world: int):
@@ -149,10 +149,9 @@ def exchange_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
     0..7) for every node, t (8..15) for the rank's destinations
     ``dst_lo:dst_hi`` (other rows' t are never read and left unset).
 
-    s of the equal node block is all-gathered (one RCCL collective of
-    ``[N, 8]``: half the bytes of gathering [s | t]); [s | t] of the
-    destination block is then computed locally into its rows (its s
-    bit-identical to the gathered one: the same per-row arithmetic).
+    ONE logits pass per rank, over its own destination block (the only rows
+    whose t it reads), then one RCCL all-gather-v of the s half (``[N, 8]``:
+    half the bytes of gathering [s | t]; blocks padded to the largest).
     ``logits_fn(lo, hi)`` -> [hi - lo, 16] replaces the HIP logits (tests)."""
     H = 8
     N = x.size(0)
@@ -161,17 +160,12 @@ def exchange_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
             return logits_rows(x, packed, lo, hi, xmax)
     if spec.world == 1:
         return logits_fn(0, N)
-    import torch.distributed as dist
-    per = (N + spec.world - 1) // spec.world
-    blk = logits_fn(spec.node_lo, spec.node_hi)
-    s_local = torch.zeros((per, H), dtype=torch.float32, device=blk.device)
-    s_local[:blk.size(0)] = blk[:, :H]
-    s_all = torch.empty((per * spec.world, H), dtype=torch.float32, device=blk.device)
-    dist.all_gather_into_tensor(s_all, s_local, group=group)
+    blk = logits_fn(spec.dst_lo, spec.dst_hi)
+    s_all = all_gather_v_rows(blk[:, :H], spec.dst_bounds, group=group)
     st = torch.empty((N, 2 * H), dtype=torch.float32, device=blk.device)
-    st[:, :H] = s_all[:N]
+    st[:, :H] = s_all
     if spec.dst_hi > spec.dst_lo:
-        st[spec.dst_lo:spec.dst_hi] = logits_fn(spec.dst_lo, spec.dst_hi)
+        st[spec.dst_lo:spec.dst_hi, H:] = blk[:, H:]
     return st
 
 

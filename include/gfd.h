@@ -280,8 +280,10 @@ gfd_status gfd_gat_logits_ex(const void* x, int x_dtype, int64_t rows, int in_fe
                              int64_t x_stride, const void* packed, int heads, int channels,
                              float* st, float* xmax, gfd_stream_t stream);
 
-/* gfd_gat_logits_ex over a whole graph (rows = destinations = num_nodes) fused
- * with the outputs of the destinations whose only message is their self loop
+/* gfd_gat_logits_ex over a whole graph (rows = destinations = num_nodes), or a
+ * contiguous destination range (x advanced to its first row, num_nodes = its
+ * length, rowptr = the range's rowptr: the destination-sharded exchange),
+ * fused with the outputs of the destinations whose only message is their self loop
  * (rowptr[i+1] - rowptr[i] == 1): their softmax has one term, so PyG's
  * out_i = mean_h W_h x_i + bias, written to out[i] (and, with stats, their
  * softmax max leaky(s_i + t_i) and denominator 1).  Other rows of out are not

@@ -9,7 +9,7 @@ is exact.  Each bench stage (bench.py ``kernels``) gets ``hbm_bytes_per_launch``
 = the sum over its kernels, keyed ``{config}:{stage}:N=..:E=..:F=..:world=..``;
 bench.py reports the dominant stage's figure as ``roofline.traffic``.
 
-usage: pmc_summary.py <fetch pass dir> <write pass dir> CONFIG N E F WORLD [tag]
+usage: GFD_TREE=<git hash> pmc_summary.py <fetch pass dir> <write pass dir> CONFIG N E F WORLD [tag]
 """
 import collections
 import csv
@@ -71,6 +71,9 @@ def main():
     for s, ks in stages.items():
         summary[f"{config}:{s}:N={N}:E={E}:F={F}:world={world}"] = {
             "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (two passes) {tag}",
+            # the git tree the passes ran on (GFD_TREE: set by the caller, the
+            # GPU box's snapshot has no .git)
+            "tree": os.environ.get("GFD_TREE", "unknown"),
             "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 128-B requests at 64 B)",
             "kernels": {k: kernels[k] for k in sorted(ks)},
             "hbm_bytes_per_launch": sum(kernels[k]["hbm_bytes_per_launch"] for k in ks),

@@ -107,6 +107,52 @@ def test_c4_dst_shards(c4, world):
         del g._shards[k]
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_multi_rank_path(world, monkeypatch):
+    """bench.Layer's N > 1 path (the one the driver's scaling run times), rank by
+    rank on this GPU with the two collectives emulated from the whole-graph
+    run: the fused logits + lone pass over the rank's destinations, the
+    all-gather-v of the source logits, the shard's tile stage.  Every rank's
+    rows equal the single-GPU layer's."""
+    import bench
+    import torch.distributed as tdist
+    from gfd import dist as gdist
+    s = bench.setup(DEV, 1_000_000, 5_000_000, 166)
+    g = s["graph"]
+    whole = bench.Layer(s, DEV, 1)
+    whole.step()
+    torch.cuda.synchronize()
+    ref, st_full, xmax = whole.out.clone(), whole.st.clone(), whole.xmax.clone()
+    bounds = gdist.edge_balanced_bounds(g.rowptr, world)
+    per = max(max(bounds[r + 1] - bounds[r] for r in range(world)), 1)
+
+    def all_gather(out, inp, group=None):
+        assert out.shape == (per * world, H) and inp.shape == (per, H)
+        for q in range(world):
+            out[q * per:q * per + bounds[q + 1] - bounds[q]] = st_full[bounds[q]:bounds[q + 1], :H]
+
+    def all_reduce(t, op=None, group=None):
+        t.copy_(torch.maximum(t, xmax))
+
+    monkeypatch.setattr(tdist, "all_gather_into_tensor", all_gather)
+    monkeypatch.setattr(tdist, "all_reduce", all_reduce)
+    for r in range(world):
+        sr = dict(s)
+        sr["spec"] = gdist.ShardSpec(g.rowptr, r, world)
+        sr["shard"] = g.shard(sr["spec"].dst_lo, sr["spec"].dst_hi)
+        layer = bench.Layer(sr, DEV, world)
+        layer.step()
+        torch.cuda.synchronize()
+        lo, hi = sr["spec"].dst_lo, sr["spec"].dst_hi
+        # [s | t] of the own rows from the fused pass: bit-identical per-row arithmetic
+        assert torch.equal(layer.st[lo:hi], st_full[lo:hi]), f"rank {r}: own logits"
+        assert_close(layer.out[:hi - lo], ref[lo:hi], atol=1e-5, rtol=1e-5,
+                     what=f"rank {r} of {world}")
+        del layer
+    for k in [k for k in g._shards if k != (0, g.num_nodes)]:
+        del g._shards[k]
+
+
 def _small(N, E, F, seed, dtype=torch.float32, pitch=None):
     from gfd import synth
     from oracle import glorot_
