@@ -21,6 +21,7 @@
 //                 backward in a second sweep.  Hub rows park u_i for:
 //   k_bwd_hub1/2  hub chunks (the forward plan's split), chunk partials summed
 //                 in a fixed order by k_sum8
+//   k_xmax        per-column maxima of |x| (the grad_W' GEMM's column scales)
 //   k_bwd_src     one wave per source (CSC), chunks for source hubs: writes
 //                 dh' = [dh (512) | ds (8) | dt (8)] per node
 //   k_gw          grad_W' = dh'^T x (528 x F) on f16 MFMA (3-term split), split-K
@@ -42,6 +43,9 @@ constexpr int kUT = 32;            // destinations per k_bwd_msg block
 constexpr int kUW = 16;            // waves per k_bwd_msg block
 constexpr int kGS = 72;            // G tile row stride (halves; 144 B rows keep 16-B loads aligned)
 constexpr int kRedBlocks = 1024;   // fixed grid of the column-sum partial kernels
+// Per-message record (64 B, edge order): alpha~ [8] | dpre [8] -- the source
+// side reads both halves of one line per message, not two lines
+constexpr int kRec = 16;
 
 __device__ __forceinline__ float ldx1(const float* p) { return *p; }
 __device__ __forceinline__ float ldx1(const uint16_t* p) { return __uint_as_float(uint32_t(*p) << 16); }
@@ -123,8 +127,8 @@ __device__ __forceinline__ float bwd_pass1(const void* __restrict__ x, int64_t l
     // lane 8 k + h <- lane 8 h + k (message k, head h)
     const float dA = __int_as_float(__builtin_amdgcn_ds_bpermute(sig, __float_as_int(sel))) * keepf;
     if (valid) {
-      dpre[int64_t(e) * 8 + h] = dA;
-      alpha_d[int64_t(e) * 8 + h] = al * keepf;
+      dpre[int64_t(e) * kRec + h] = dA;
+      alpha_d[int64_t(e) * kRec + h] = al * keepf;
       adot = fmaf(al, dA, adot);
     }
   }
@@ -178,8 +182,8 @@ __device__ __forceinline__ float bwd_single(const void* __restrict__ x, int64_t 
   const float adot = sum_xor8_16_32(valid ? al * dA : 0.f);
   const float dd = valid ? al * (dA - adot) * (pre > 0.f ? 1.0f : slope) : 0.f;
   if (valid) {
-    dpre[int64_t(e) * 8 + h] = dd;
-    alpha_d[int64_t(e) * 8 + h] = al * keepf;
+    dpre[int64_t(e) * kRec + h] = dd;
+    alpha_d[int64_t(e) * kRec + h] = al * keepf;
   }
   return sum_xor8_16_32(dd);
 }
@@ -250,8 +254,8 @@ __device__ __forceinline__ void bwd_pair(const void* __restrict__ x, int64_t ldx
     const float adot = sum_xor8_16_32(valid ? al * dA : 0.f);
     const float dd = valid ? al * (dA - adot) * (pre[d] > 0.f ? 1.0f : slope) : 0.f;
     if (valid) {
-      dpre[int64_t(e) * 8 + h] = dd;
-      alpha_d[int64_t(e) * 8 + h] = al * keepf;
+      dpre[int64_t(e) * kRec + h] = dd;
+      alpha_d[int64_t(e) * kRec + h] = al * keepf;
     }
     const float dts = sum_xor8_16_32(dd);
     if (lane < 8) dt[int64_t(dsc[d].x) * 8 + lane] = dts;
@@ -272,7 +276,7 @@ __device__ __forceinline__ float bwd_pass2(const int32_t* __restrict__ col, int 
       const int j = col[e];
       const float pre = st[int64_t(j) * 16 + h] + t_h;
       const float al = __expf(leaky(pre, slope) - m_h) * inv_h;
-      float* dp = dpre + int64_t(e) * 8 + h;
+      float* dp = dpre + int64_t(e) * kRec + h;
       const float d = al * (*dp - adot) * (pre > 0.f ? 1.0f : slope);
       *dp = d;
       dts += d;
@@ -397,8 +401,8 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
       const int e = dsc[d].y;
       float keepf = 1.0f;
       if (dp > 0.f) keepf = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? keep : 0.f;
-      dpre[int64_t(e) * 8 + h] = 0.f;
-      alpha_d[int64_t(e) * 8 + h] = keepf;
+      dpre[int64_t(e) * kRec + h] = 0.f;
+      alpha_d[int64_t(e) * kRec + h] = keepf;
       dt[int64_t(dsc[d].x) * 8 + h] = 0.f;
     }
     return;
@@ -604,8 +608,8 @@ __device__ __forceinline__ void src_segment(const int32_t* __restrict__ csc_dst,
     const int pc = valid ? p : p1 - 1;
     const int e = csc_eid[pc];
     const int i = csc_dst[pc];
-    const float a = valid ? alpha_d[int64_t(e) * 8 + h] : 0.f;
-    ds += valid ? dpre[int64_t(e) * 8 + h] : 0.f;
+    const float a = valid ? alpha_d[int64_t(e) * kRec + h] : 0.f;
+    ds += valid ? dpre[int64_t(e) * kRec + h] : 0.f;
     const int nk = min(8, p1 - b);
     float gv[8];
 #pragma unroll
@@ -622,14 +626,16 @@ __device__ __forceinline__ void src_segment(const int32_t* __restrict__ csc_dst,
   }
 }
 
-// Per-column maxima of |dh'| (the grad_W' GEMM's A operand) and |x| (its B
-// operand) and each dh' row's power-of-two exponent (grad_x's A operand): the
-// fp16 3-term GEMMs scale every column (row) on its own, so a heavy-tailed
-// feature or gradient column does not push the others into fp16 subnormals.
+// Per-column maxima of |dh'| (the grad_W' GEMM's A operand; k_bwd_src) and |x|
+// (its B operand; k_xmax) and each dh' row's power-of-two exponent (grad_x's A
+// operand; k_bwd_src): the fp16 3-term GEMMs scale every column (row) on its
+// own, so a heavy-tailed feature or gradient column does not push the others
+// into fp16 subnormals.
 // amax[m] (m < kDH): dh' column m; amax[kDH + f]: x column f, as float bits
 // (non-negative floats order like their bits: an integer max is exact and
 // order-independent).  kAmaxCols = kDH + 256 words.
-constexpr int kAmaxCols = kDH + 256;
+constexpr int kXCols = 256;  // x columns (F <= 256)
+constexpr int kAmaxCols = kDH + kXCols;
 
 __device__ __forceinline__ void amax_put(uint32_t* __restrict__ amax, int c, float v) {
   const uint32_t bits = __float_as_uint(v);
@@ -638,18 +644,16 @@ __device__ __forceinline__ void amax_put(uint32_t* __restrict__ amax, int c, flo
   if (bits > __atomic_load_n(amax + c, __ATOMIC_RELAXED)) atomicMax(amax + c, bits);
 }
 
-// dh' row j from y (lane = channel), ds (head lane & 7, complete) and dt_j;
+// dh' row j from y (lane = channel), ds and dt_j (head lane & 7, complete);
 // folds |value| into the lane's per-column maxima (cm[hh]: column hh C +
 // lane; ct[0 / 1]: columns HC + lane / HC + H + lane, lanes < 8) and returns
 // the row's max |value| (every lane).
-__device__ __forceinline__ float write_dh(int64_t j, const float (&y)[H], float ds,
-                                          const float* __restrict__ dt,
+__device__ __forceinline__ float write_dh(int64_t j, const float (&y)[H], float ds, float dtl,
                                           const float* __restrict__ att_src,
                                           const float* __restrict__ att_dst,
                                           float* __restrict__ dh, float (&cm)[H], float (&ct)[2]) {
   const int lane = threadIdx.x & 63;
   float* r = dh + j * kDH;
-  const float dtl = dt[j * 8 + (lane & 7)];
   float mx = 0.f;
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
@@ -671,13 +675,11 @@ __device__ __forceinline__ float write_dh(int64_t j, const float (&y)[H], float 
   return max_wave(mx);
 }
 
-// Block-level per-column maxima (the block's waves' in LDS), then one
-// conditional atomic per column.  cm / ct as write_dh, xm[q]: x column
-// lane + 64 q (q < 4, F <= 256).
+// Block-level per-column maxima of dh' (the block's waves' in LDS), then one
+// conditional atomic per column.  cm / ct as write_dh.
 __device__ __forceinline__ void amax_commit(const float (&cm)[H], const float (&ct)[2],
-                                            const float (&xm)[4], int F,
                                             uint32_t* __restrict__ amax) {
-  __shared__ float red[4][kAmaxCols];  // 256-thread blocks
+  __shared__ float red[4][kDH];  // 256-thread blocks
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) red[w][hh * C + lane] = cm[hh];
@@ -685,47 +687,81 @@ __device__ __forceinline__ void amax_commit(const float (&cm)[H], const float (&
     red[w][HC + lane] = ct[0];
     red[w][HC + H + lane] = ct[1];
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) red[w][kDH + lane + 64 * q] = xm[q];
   __syncthreads();
-  for (int c = threadIdx.x; c < kDH + F; c += blockDim.x) {
-    float m = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) m = fmaxf(m, red[k][c]);
-    amax_put(amax, c, m);
-  }
+  for (int c = threadIdx.x; c < kDH; c += blockDim.x)
+    amax_put(amax, c, fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c])));
 }
 
-template <typename XT>
 __global__ void __launch_bounds__(256) k_bwd_src(
     const int32_t* __restrict__ colptr, const int32_t* __restrict__ csc_dst,
     const int32_t* __restrict__ csc_eid, int64_t N, const int32_t* __restrict__ src_hub_rank,
     const float* __restrict__ alpha_d, const float* __restrict__ dpre,
     const float* __restrict__ dt, const float* __restrict__ g, const float* __restrict__ att_src,
-    const float* __restrict__ att_dst, const typename XT::T* __restrict__ x, int F, int64_t ldx,
-    float* __restrict__ dh, uint32_t* __restrict__ amax, int32_t* __restrict__ erow) {
+    const float* __restrict__ att_dst, float* __restrict__ dh, uint32_t* __restrict__ amax,
+    int32_t* __restrict__ erow) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  float cm[H], ct[2] = {0.f, 0.f}, xm[4] = {0.f, 0.f, 0.f, 0.f};
+  float cm[H], ct[2] = {0.f, 0.f};
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) cm[hh] = 0.f;
   for (int64_t j = w0; j < N; j += nw) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = lane + 64 * q;
-      if (f < F) xm[q] = fmaxf(xm[q], fabsf(ldx1(x + j * ldx + f)));
-    }
     if (src_hub_rank && src_hub_rank[j] >= 0) continue;  // k_bwd_src_hub
+    const float dtl = dt[j * 8 + (lane & 7)];
     float y[H];
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) y[hh] = 0.f;
     float ds = 0.f;
     src_segment(csc_dst, csc_eid, colptr[j], colptr[j + 1], alpha_d, dpre, g, y, ds);
-    const float rm = write_dh(j, y, sum_xor8_16_32(ds), dt, att_src, att_dst, dh, cm, ct);
+    const float rm = write_dh(j, y, sum_xor8_16_32(ds), dtl, att_src, att_dst, dh, cm, ct);
     if (lane == 0) erow[j] = scale_exp(rm);
   }
-  amax_commit(cm, ct, xm, F, amax);
+  amax_commit(cm, ct, amax);
+}
+
+// Per-column maxima of |x| (amax[kDH + f]): one wave per row in a grid-stride
+// loop, lane = 4-column chunk (16-B fp32 / 8-B bf16 loads when rows allow
+// them, VEC; else one column per lane and q), four rows' loads in flight;
+// block maxima in LDS, then one conditional atomic per column.
+template <typename XT, bool VEC>
+__global__ void __launch_bounds__(256) k_xmax(const typename XT::T* __restrict__ x, int64_t N,
+                                              int F, int64_t ldx, uint32_t* __restrict__ amax) {
+  __shared__ float red[4][kXCols];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nw = int64_t(gridDim.x) * 4;
+  // VEC: columns 4 lane + q; else lane + 64 q
+  auto col = [&](int q) { return VEC ? 4 * lane + q : lane + 64 * q; };
+  auto row4 = [&](int64_t j) {
+    f32x4 v;
+    if (VEC && 4 * lane + 3 < F) {
+      v = load4<XT>(x + j * ldx + 4 * lane);
+    } else {  // (a ragged last chunk: columns past F are neither read nor counted)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = col(q) < F ? ldx1(x + j * ldx + col(q)) : 0.f;
+    }
+    return v;
+  };
+  f32x4 xm = {0.f, 0.f, 0.f, 0.f};
+  int64_t j = int64_t(blockIdx.x) * 4 + w;
+  for (; j + 3 * nw < N; j += 4 * nw) {
+    f32x4 v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = row4(j + r * nw);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xm[q] = fmaxf(xm[q], fabsf(v[r][q]));
+  }
+  for (; j < N; j += nw) {
+    const f32x4 v = row4(j);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xm[q] = fmaxf(xm[q], fabsf(v[q]));
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[w][col(q)] = xm[q];  // col(q) < 256 = kXCols
+  __syncthreads();
+  for (int f = threadIdx.x; f < F; f += blockDim.x)
+    amax_put(amax, kDH + f, fmaxf(fmaxf(red[0][f], red[1][f]), fmaxf(red[2][f], red[3][f])));
 }
 
 // source hub chunks {hub, p0, p1, src}: partial y (512) | ds (8) per chunk
@@ -799,7 +835,7 @@ __global__ void __launch_bounds__(512) k_bwd_src_hub2(
 // ---------------------------------------------------------------------------
 // grad_W' = dh'^T x  ([528, F], a sum over all N nodes) on f16 MFMA
 // 16x16x32 with the forward's 3-term split: both operands scaled by one power
-// of two each (max |dh'| and max |x| -> [2^13, 2^14), collected by k_bwd_src),
+// of two each (max |dh'| and max |x| -> [2^13, 2^14), collected by k_bwd_src / k_xmax),
 // v = hi + lo in f16, acc += hi.hi + hi.lo + lo.hi (~2^-21 relative per
 // product; an fp32 MFMA 16x16x4 does 1/16 of the work per cycle).
 //  * block (8 waves) = one 176-row m-block of dh' x all Fu <= 256 feature
@@ -1160,18 +1196,49 @@ __global__ void __launch_bounds__(1024) k_reduce_few(const float* __restrict__ p
   }
 }
 
-// column sums of a [n, 64] fp32 matrix: fixed-grid partials part[block][64]
+// column sums of a [n, 64] fp32 matrix: fixed-grid partials part[block][64].
+// A wave reads 4 rows per 16-B-per-lane load (lane = row (lane >> 4), columns
+// 4 (lane & 15) ..), four such loads in flight per iteration, each into its
+// own accumulator; fixed summation order.
 __global__ void __launch_bounds__(256) k_colsum64(const float* __restrict__ a, int64_t n,
                                                   float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float s = 0.f;
-  for (int64_t r = int64_t(blockIdx.x) * 4 + w; r < n; r += int64_t(gridDim.x) * 4)
-    s += a[r * C + lane];
-  red[w][lane] = s;
+  __shared__ float4 red[4][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane & 15;
+  const int64_t st = int64_t(gridDim.x) * 16;  // rows per sweep of the grid
+  int64_t r = (int64_t(blockIdx.x) * 4 + w) * 4 + (lane >> 4);
+  float4 s[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (; r + 3 * st < n; r += 4 * st) {
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = reinterpret_cast<const float4*>(a + (r + k * st) * C)[q];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s[k].x += v[k].x; s[k].y += v[k].y; s[k].z += v[k].z; s[k].w += v[k].w;
+    }
+  }
+  for (; r < n; r += st) {  // at most three rows left
+    const float4 v = reinterpret_cast<const float4*>(a + r * C)[q];
+    s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
+  }
+  float4 t;
+  t.x = (s[0].x + s[1].x) + (s[2].x + s[3].x);
+  t.y = (s[0].y + s[1].y) + (s[2].y + s[3].y);
+  t.z = (s[0].z + s[1].z) + (s[2].z + s[3].z);
+  t.w = (s[0].w + s[1].w) + (s[2].w + s[3].w);
+#pragma unroll
+  for (int m = 16; m <= 32; m <<= 1) {  // the wave's 4 rows of each column group
+    t.x += __shfl_xor(t.x, m); t.y += __shfl_xor(t.y, m);
+    t.z += __shfl_xor(t.z, m); t.w += __shfl_xor(t.w, m);
+  }
+  if (lane < 16) red[w][q] = t;
   __syncthreads();
-  if (threadIdx.x < 64)
-    part[int64_t(blockIdx.x) * 64 + lane] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (threadIdx.x < 64) {
+    const float* rf = reinterpret_cast<const float*>(red);
+    part[int64_t(blockIdx.x) * 64 + lane] =
+        ((rf[lane] + rf[64 + lane]) + rf[128 + lane]) + rf[192 + lane];
+  }
 }
 
 // grad_att_src[h][c] = sum_f W[h C + c][f] S_h[f] (rows HC.. of gw'), att_dst from T
@@ -1201,7 +1268,7 @@ int gw_slabs(int64_t N) {
 int kf_fu(int F) { return (F + 63) / 64; }
 
 struct BwdLayout {
-  size_t whdr, amax, erow, bhi, blo, dpre, alpha, dt, uhub, cpart, hadot, spart, dh, slab, gw, gbp;
+  size_t whdr, amax, erow, bhi, blo, rec, dt, uhub, cpart, hadot, spart, dh, slab, gw, gbp;
 };
 
 BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
@@ -1216,8 +1283,7 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
   L.erow = take(sizeof(int32_t) * size_t(N));
   L.bhi = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
   L.blo = take(sizeof(uint4) * size_t(H) * 2 * NT * 64);
-  L.dpre = take(sizeof(float) * size_t(M) * 8);
-  L.alpha = take(sizeof(float) * size_t(M) * 8);
+  L.rec = take(sizeof(float) * size_t(M) * kRec);
   L.dt = take(sizeof(float) * size_t(N) * 8);
   L.uhub = take(sizeof(float) * size_t(hubs > 0 ? hubs : 0) * H * Fu);
   L.cpart = take(sizeof(float) * size_t(ch) * 8);
@@ -1305,8 +1371,8 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   int32_t* erow = reinterpret_cast<int32_t*>(b + L.erow);
   uint4* bhi = reinterpret_cast<uint4*>(b + L.bhi);
   uint4* blo = reinterpret_cast<uint4*>(b + L.blo);
-  float* dpre = reinterpret_cast<float*>(b + L.dpre);
-  float* alpha_d = reinterpret_cast<float*>(b + L.alpha);
+  float* alpha_d = reinterpret_cast<float*>(b + L.rec);  // record words 0..7
+  float* dpre = alpha_d + H;                               // record words 8..15
   float* dt = reinterpret_cast<float*>(b + L.dt);
   float* uhub = reinterpret_cast<float*>(b + L.uhub);
   float* cpart = reinterpret_cast<float*>(b + L.cpart);
@@ -1334,9 +1400,17 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
     int64_t blocks = (N + 3) / 4;
     if (blocks > 16384) blocks = 16384;
     GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
-    k_bwd_src<XT><<<unsigned(blocks), 256, 0, stream>>>(
+    const bool xvec = ldx % 4 == 0 &&
+                      reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
+    const unsigned xb = unsigned(blocks < 2048 ? blocks : 2048);
+    if (xvec)
+      k_xmax<XT, true><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
+    else
+      k_xmax<XT, false><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
+    GFD_LAUNCH_CHECK();
+    k_bwd_src<<<unsigned(blocks), 256, 0, stream>>>(
         colptr, csc_dst, csc_eid, N, shubs > 0 ? src_plan->hub_rank : nullptr, alpha_d, dpre, dt,
-        g, att_src, att_dst, x, F, ldx, dh, amax, erow);
+        g, att_src, att_dst, dh, amax, erow);
     GFD_LAUNCH_CHECK();
     if (shubs > 0) {
       k_bwd_src_hub1<<<unsigned((schunks + 3) / 4), 256, 0, stream>>>(
@@ -1421,6 +1495,7 @@ gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ld
       ldx < F)
     return GFD_ERR_ARGUMENT;
   if (!(dp >= 0.f && dp < 1.f)) return GFD_ERR_ARGUMENT;
+  if (reinterpret_cast<uintptr_t>(g) % 16 != 0) return GFD_ERR_ARGUMENT;  // k_colsum64
   if (N > 0x7fffffff || M > 0x7fffffff || ldx * (x_dtype == GFD_DTYPE_BF16 ? 2 : 4) > 0xffffffffLL)
     return GFD_ERR_UNSUPPORTED;
   if (plan && plan->num_hubs > 0 && (!plan->hub_rank || !plan->hub_chunk || !plan->hub_chunk_ptr ||

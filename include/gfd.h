@@ -409,7 +409,8 @@ gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t num_nodes, i
  * GATConv backward (autograd of the PyG dataflow at loss.backward(),
  * train.py:142).  Given grad_out [N, C], the forward's
  * st [N, 2H] and stats [N, 2H], writes grad_x [N, F] (nullable), grad_weight
- * [H*C, F], grad_att_src/grad_att_dst [H*C], grad_bias [C] (nullable).  All
+ * [H*C, F], grad_att_src/grad_att_dst [H*C], grad_bias [C] (nullable); grad_out
+ * contiguous and 16-B aligned.  All
  * outputs are overwritten (not accumulated); deterministic (no float atomics).
  * Like the forward it gathers x rows, never the projected rows: the attention
  * gradient is <W_h^T grad_out_i / H, x_j>.  ``plan`` is the forward's plan

@@ -42,8 +42,10 @@ def al(o): return (o + 255) // 256 * 256
 Fu = (F + 15) // 16 * 16; NT = Fu // 16
 o = 0
 offs = {}
-for name, nb in (("whdr", 64), ("amax", 64), ("bhi", 16 * H * 2 * NT * 64), ("blo", 16 * H * 2 * NT * 64),
-                 ("dpre", 4 * M * 8), ("alpha", 4 * M * 8), ("dt", 4 * N * 8),
+# mirrors bwd_layout() in gfd_gat_bwd.hip
+for name, nb in (("whdr", 64), ("amax", 4 * (528 + 256)), ("erow", 4 * N),
+                 ("bhi", 16 * H * 2 * NT * 64), ("blo", 16 * H * 2 * NT * 64),
+                 ("rec", 4 * M * 16), ("dt", 4 * N * 8),
                  ("uhub", 4 * plan.num_hubs * H * Fu), ("cpart", 4 * plan.num_chunks * 8), ("hadot", 4 * plan.num_hubs * 8),
                  ("spart", 4 * splan.num_chunks * 520), ("dh", 4 * N * 528)):
     o = al(o); offs[name] = o; o += nb
