@@ -430,7 +430,13 @@ def main():
             res["cpu_baseline"] = cpu_baseline(s, args)
         if "c4bwd" in want:
             log("[bench] leg C4 forward + backward ...")
-            legs["c4_layer_fwd_bwd"] = bench_legs.c4_layer_fwd_bwd(s, dev)
+            leg = bench_legs.c4_layer_fwd_bwd(s, dev)
+            pmc_b = load_pmc(args.pmc, f"c4:backward:N={N}:world=1")
+            if pmc_b:  # the backward kernels' HBM bytes (scripts/pmc_bwd_summary.py)
+                leg["roofline"]["traffic"] = pmc_b.get("hbm_bytes_per_pass")
+                leg["roofline"]["traffic_source"] = {"tree": pmc_b.get("tree"),
+                                                     "source": pmc_b.get("source")}
+            legs["c4_layer_fwd_bwd"] = leg
         if "sample" in want:
             log("[bench] leg neighbour sampling on the C4 graph ...")
             legs["neighbor_sampling"] = bench_legs.neighbor_sampling(s, dev)

@@ -32,6 +32,8 @@ import time
 
 import torch
 
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (as bench.py)
+
 H, C = 8, 64
 
 
@@ -154,10 +156,33 @@ def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2):
     fwd_med, _ = _time(lambda: fwd(), steps, warmup)
     med, mean = _time(fwd_bwd, steps, warmup)
     E = s["graph"].num_messages - s["graph"].num_nodes
+    bwd_ms = med - fwd_med
+    nbytes = bwd_algorithmic_bytes(g.num_nodes, g.num_messages, s["x"].shape[1],
+                                   s["x"].element_size())
     return {"workload": f"C4 GATConv layer 0 forward (training stats) + backward (grad W, att, "
                         f"bias; no grad_x), N={g.num_nodes} E={E}", "unit": "edges/s",
             "value": E / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
-            "forward_ms": fwd_med, "backward_ms": med - fwd_med}
+            "forward_ms": fwd_med, "backward_ms": bwd_ms,
+            # the whole backward pass against HBM: its algorithmic bytes (DESIGN.md
+            # §5, bwd_algorithmic_bytes) over backward_ms (one C-ABI call; its
+            # kernels' split is in profiles/r3c_bwd_kernel_top25.txt)
+            "roofline": {"bound": "hbm", "scope": "backward pass", "achieved":
+                         nbytes / (bwd_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": nbytes / (bwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         "algorithmic_bytes": nbytes, "traffic": None}}
+
+
+def bwd_algorithmic_bytes(N, M, F, es, C=64, kdh=528):
+    """Minimum HBM bytes of one GATConv backward (grad W, att, bias) in this
+    formulation: per message (M, self loops included) the x_j row, its index
+    and source logits and the 64-B record written (k_bwd_msg), then the CSC
+    entry, the record and the g_i row (k_bwd_src); per node the g row, logits
+    and softmax stats, dt (k_bwd_msg), the x row (k_xmax), the dh' row written
+    (k_bwd_src) and read with the x row (k_gw), the g row again (grad_bias)."""
+    per_msg = (es * F + 4 + 32 + 64) + (8 + 64 + 4 * C)
+    per_node = (4 * C + 32 + 64 + 32) + es * F + (4 + 32 + 4 * kdh + 4) + \
+        (4 * kdh + es * F) + 4 * C
+    return float(M) * per_msg + float(N) * per_node
 
 
 def temporal_snapshots(dev, steps=20, warmup=3, cpu_runs=3):
