@@ -247,6 +247,35 @@ def test_nan_row_padding_and_last_row_at_allocation_end(F):
     assert_close(out, _oracle(x, ei, W, a_s, a_d, b), what=f"NaN padding F={F}")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("F", [100, 166])
+def test_backward_nan_row_padding_and_last_row_at_allocation_end(F, dtype):
+    """The backward over the same padded x (row pitch > F, NaN padding, the last
+    row ending at the end of its allocation): the per-column x maxima (k_xmax,
+    16-B / 8-B chunks, a ragged last chunk read element by element) and the
+    grad_W' GEMM's x tiles never read or count the padding.  grad_W, grad_att
+    and grad_bias against the fp32 oracle's autograd on the same (rounded) x."""
+    from _util import assert_close_scaled
+    from gfd.nn import gat_conv
+    from oracle import gatconv_forward
+    N = 5000
+    ei, x, W, a_s, a_d, b = _small(N, 40000, F, seed=16)
+    x = x.to(dtype)
+    ldx = (F + 7) // 8 * 8 + 8
+    buf = torch.full((N * ldx - (ldx - F),), float("nan"), device=DEV, dtype=dtype)
+    xv = buf.as_strided((N, F), (ldx, 1))
+    xv.copy_(x.to(DEV))
+    g = torch.randn(N, C, generator=torch.Generator().manual_seed(9))
+    ps = [t.to(DEV).requires_grad_(True) for t in (W, a_s, a_d, b)]
+    (gat_conv(xv, ei.to(DEV), *ps) * g.to(DEV)).sum().backward()
+    pr = [t.clone().requires_grad_(True) for t in (W, a_s, a_d, b)]
+    (gatconv_forward(x.float(), ei, *pr) * g).sum().backward()
+    for name, u, v in zip(("W", "att_src", "att_dst", "bias"), ps, pr):
+        assert torch.isfinite(u.grad).all(), f"grad_{name}: non-finite (padding read)"
+        assert_close_scaled(u.grad.reshape(v.grad.shape), v.grad,
+                            what=f"grad_{name}, NaN padding F={F} {dtype}")
+
+
 @pytest.mark.parametrize("order,cap", [(False, None), (True, 2), (True, 4)])
 def test_plan_orders_that_are_not_degree_sorted(order, cap):
     """Class boundaries are exact for any slot order: no order at all, and an
