@@ -431,7 +431,7 @@ def main():
         if "c4bwd" in want:
             log("[bench] leg C4 forward + backward ...")
             leg = bench_legs.c4_layer_fwd_bwd(s, dev)
-            pmc_b = load_pmc(args.pmc, f"c4:backward:N={N}:world=1")
+            pmc_b = load_pmc(args.pmc, f"c4:backward:N={s['graph'].num_nodes}:world=1")
             if pmc_b:  # the backward kernels' HBM bytes (scripts/pmc_bwd_summary.py)
                 leg["roofline"]["traffic"] = pmc_b.get("hbm_bytes_per_pass")
                 leg["roofline"]["traffic_source"] = {"tree": pmc_b.get("tree"),
