@@ -437,6 +437,8 @@ def main():
                 leg["roofline"]["traffic_source"] = {"tree": pmc_b.get("tree"),
                                                      "source": pmc_b.get("source")}
             legs["c4_layer_fwd_bwd"] = leg
+            log("[bench] leg C4 forward + backward, attention dropout 0.2 ...")
+            legs["c4_layer_fwd_bwd_dropout"] = bench_legs.c4_layer_fwd_bwd(s, dev, dropout=0.2)
         if "sample" in want:
             log("[bench] leg neighbour sampling on the C4 graph ...")
             legs["neighbor_sampling"] = bench_legs.neighbor_sampling(s, dev)

@@ -135,8 +135,10 @@ def c3_tgn_49_steps(dev, steps=20, warmup=3):
             "ms_mean": mean}
 
 
-def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2):
-    """GATConv forward + backward on the C4 workload ``s`` (bench.setup)."""
+def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2, dropout=0.0):
+    """GATConv forward + backward on the C4 workload ``s`` (bench.setup);
+    ``dropout`` > 0: the reference's training configuration (attention dropout
+    0.2, config.py:35), which keeps the class schedule (counter-based masks)."""
     from gfd.nn import gat_conv
     W = s["W"].clone().requires_grad_(True)
     a_s = s["a_s"].clone().requires_grad_(True)
@@ -147,7 +149,7 @@ def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2):
     g.csc()
 
     def fwd():
-        return gat_conv(s["x"], g, W, a_s, a_d, b, training=True)
+        return gat_conv(s["x"], g, W, a_s, a_d, b, dropout=dropout, training=True)
 
     def fwd_bwd():
         out = fwd()
@@ -160,7 +162,8 @@ def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2):
     nbytes = bwd_algorithmic_bytes(g.num_nodes, g.num_messages, s["x"].shape[1],
                                    s["x"].element_size())
     return {"workload": f"C4 GATConv layer 0 forward (training stats) + backward (grad W, att, "
-                        f"bias; no grad_x), N={g.num_nodes} E={E}", "unit": "edges/s",
+                        f"bias; no grad_x), N={g.num_nodes} E={E}, attention dropout {dropout}",
+            "unit": "edges/s",
             "value": E / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
             "forward_ms": fwd_med, "backward_ms": bwd_ms,
             # the whole backward pass against HBM: its algorithmic bytes (DESIGN.md

@@ -18,7 +18,8 @@
 //                 holds u_i (8 x F) in registers and walks its destinations'
 //                 messages: x_j gathered once (664 B at F = 166, not the 2 KB
 //                 h_j row), 8 head dots, a transposing 64-lane reduce, softmax
-//                 backward in a second sweep.  Hub rows park u_i for:
+//                 backward in a second sweep; per message a 64-B record
+//                 (alpha~ | dpre).  Hub rows park u_i for:
 //   k_bwd_hub1/2  hub chunks (the forward plan's split), chunk partials summed
 //                 in a fixed order by k_sum8
 //   k_xmax        per-column maxima of |x| (the grad_W' GEMM's column scales)
@@ -27,7 +28,8 @@
 //   k_gw          grad_W' = dh'^T x (528 x F) on f16 MFMA (3-term split), split-K
 //                 slabs + ordered reduce
 //   k_att_grad    grad_att from the S / T rows of grad_W'
-//   k_gemm        grad_x = dh W (only when requested)
+//   k_colsum64    grad_bias = column sums of g (fixed-grid partials)
+//   k_gx / k_gemm grad_x = dh W (only when requested; f16 MFMA for F <= 64)
 // Deterministic: no float atomics anywhere; every sum has a fixed order.
 #include "gfd_check.h"
 #include "gfd_fwd.h"
