@@ -87,6 +87,8 @@ class GATConvFunction(torch.autograd.Function):
         slope, dp, seed, has_bias = ctx.meta
         dev = x.device
         g = grad_out.contiguous().to(torch.float32)
+        if g.data_ptr() % 16:  # the C-ABI reads grad_out rows as 16-B vectors
+            g = g.clone()
         N, F = x.shape
         H, C = SUPPORTED_HEADS, weight.size(0) // SUPPORTED_HEADS
         csc = graph.csc()
