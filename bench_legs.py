@@ -100,7 +100,7 @@ def c1_gat2_forward(dev, steps=20, warmup=3, cpu_runs=3):
             "max_abs_err_vs_oracle": err}
 
 
-def c2_gat3_train_step(dev, steps=20, warmup=3):
+def c2_gat3_train_step(dev, steps=20, warmup=3, cpu_runs=3):
     d = _elliptic(dev)
     m = _model("gat", 165, 3, dev).train()
     opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=5e-4)
@@ -117,22 +117,68 @@ def c2_gat3_train_step(dev, steps=20, warmup=3):
 
     med, mean = _time(step, steps, warmup)
     fwd_med, _ = _time(lambda: m(d["x"], d["edge_index"]), steps, warmup)
+    # CPU baseline: the same step with the oracle's PyG-dataflow model on the
+    # host (train.py:105-143's loop body), same weights, 1 warm-up + median
+    from oracle import GATRef
+    ref = GATRef(165, 64, 1, num_layers=3).train()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=True)
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3, weight_decay=5e-4)
+    rcrit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0]))
+    xc, ec, mc, ylc = d["x"].cpu(), d["edge_index"].cpu(), mask.cpu(), yl.cpu()
+    times = []
+    for _ in range(1 + cpu_runs):
+        t0 = time.perf_counter()
+        ropt.zero_grad()
+        rl = rcrit(ref(xc, ec)[mc].squeeze(1), ylc)
+        rl.backward()
+        ropt.step()
+        times.append(time.perf_counter() - t0)
+    tt = sorted(times[1:])
     return {"workload": f"GAT 3 layers train step (fwd + BCE(pos_weight 50) + bwd + Adam), "
                         f"Elliptic-shaped N={d['N']} E={d['E']} F=165, dropout 0.2",
             "unit": "edges/s", "value": d["E"] / (med * 1e-3), "ms_per_step": med,
-            "ms_mean": mean, "forward_ms_train_mode": fwd_med}
+            "ms_mean": mean, "forward_ms_train_mode": fwd_med,
+            "cpu_baseline": {"value": d["E"] / tt[len(tt) // 2], "unit": "edges/s",
+                             "median_s": tt[len(tt) // 2], "min_s": tt[0], "runs": cpu_runs,
+                             "cores": torch.get_num_threads(), "kind": "port",
+                             "sample": "the whole C2 graph: oracle GATRef train step (PyG CPU "
+                                       "dataflow + torch autograd + Adam), same weights"}}
 
 
-def c3_tgn_49_steps(dev, steps=20, warmup=3):
+def c3_tgn_49_steps(dev, steps=20, warmup=3, cpu_runs=3):
     d = _elliptic(dev)
     m = _model("tgn", 165, 3, dev).eval()
     with torch.no_grad():
         med, mean = _time(lambda: m.forward_snapshots(d["x"], d["edge_index"], d["time_step"]),
                           steps, warmup)
+    # CPU baseline: the reference's per-step loop -- extract each snapshot
+    # (dataset.py:198-240, oracle temporal_subgraph_ref) and run the oracle's
+    # TemporalGNN on it with h0 = 0 (tgn.py:88-89), same weights
+    from oracle import TemporalGNNRef
+    from oracle.temporal_ref import temporal_subgraph_ref
+    ref = TemporalGNNRef(165, 64, 1, num_layers=3).eval()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=True)
+    xc = d["x"].cpu()
+    ts, ei = d["time_step"].cpu().numpy(), d["edge_index"].cpu().numpy()
+    t0s, t1s = int(ts.min()), int(ts.max())
+    times = []
+    with torch.no_grad():
+        for _ in range(1 + cpu_runs):
+            c0 = time.perf_counter()
+            for t in range(t0s, t1s + 1):
+                nodes, loc, _ = temporal_subgraph_ref(ts, ei, t)
+                ref(xc[torch.from_numpy(nodes)], torch.from_numpy(loc))
+            times.append(time.perf_counter() - c0)
+    tt = sorted(times[1:])
     return {"workload": f"TemporalGNN 3 layers, forward over the 49 time-step snapshots "
                         f"(h0 = 0 per step), N={d['N']} E={d['E']} F=165, eval",
             "unit": "edges/s", "value": d["E"] / (med * 1e-3), "ms_per_step": med,
-            "ms_mean": mean}
+            "ms_mean": mean,
+            "cpu_baseline": {"value": d["E"] / tt[len(tt) // 2], "unit": "edges/s",
+                             "median_s": tt[len(tt) // 2], "min_s": tt[0], "runs": cpu_runs,
+                             "cores": torch.get_num_threads(), "kind": "port",
+                             "sample": "the whole C3 workload: per step snapshot extraction "
+                                       "(numpy) + oracle TemporalGNNRef (PyG CPU dataflow)"}}
 
 
 def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2, dropout=0.0):
