@@ -49,7 +49,8 @@ def log(*a):
 
 def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); > 1 without torchrun launches them itself")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", choices=["c4", "c5"], default="c4")
@@ -121,17 +122,17 @@ class Layer:
         self.plan = s["shard"].plan
         self.packed = torch.empty(self.lib.gfd_gat_packed_size(F, H, C), dtype=torch.uint8,
                                   device=dev)
+        # whole graph: one [N, 16] logits table.  A shard (N > 1, or the tests'
+        # virtual shards): the split layout of gfd_gat_aggregate_split -- s of
+        # every node in s_all [N, 8] (rank r's rows at its destination block,
+        # so the all-gather-v of the source logits writes straight into the
+        # table the kernels read: no scatter between collective and kernels),
+        # t of the own destinations in t_loc [n_dst, 8]
         self.st = torch.empty((self.N, 2 * H), dtype=torch.float32, device=dev)
-        # sharded (N > 1, or the tests' virtual shards): one fused logits + lone
-        # pass over the rank's own destinations; at N > 1 their source half is
-        # all-gathered-v (gfd.dist.exchange_logits: [N, 8] instead of [N, 16])
-        sizes = [spec.dst_bounds[r + 1] - spec.dst_bounds[r] for r in range(world)]
-        self.per = max(max(sizes), 1)
-        self.sizes = sizes
-        self.st_local = torch.empty((max(self.per, self.n_dst, 1), 2 * H), dtype=torch.float32,
-                                    device=dev)
-        self.s_local = torch.zeros((self.per, H), dtype=torch.float32, device=dev)
-        self.s_all = torch.empty((self.per * world, H), dtype=torch.float32, device=dev)
+        self.s_all = torch.empty((self.N, H), dtype=torch.float32, device=dev)
+        self.t_loc = torch.empty((max(self.n_dst, 1), H), dtype=torch.float32, device=dev)
+        b = spec.dst_bounds
+        self.s_blocks = [self.s_all[b[r]:b[r + 1]] for r in range(world)]
         self.out = torch.empty((max(self.n_dst, 1), C), dtype=torch.float32, device=dev)
         self.ws = torch.empty(self.lib.gfd_gat_fwd_workspace_size(
             self.N, self.n_dst, F, H, C, self.plan.num_hubs, self.plan.num_chunks),
@@ -143,7 +144,7 @@ class Layer:
         # (gfd_gat_logits_lone over the rank's destinations) and the tile stage
         # skips that class -- whole graph or shard, at every world size
         self.whole = spec.dst_lo == 0 and spec.dst_hi == self.N and world == 1
-        self.stages = self.STAGES_FUSED
+        self.stages = self.STAGES_FUSED if world == 1 else self.STAGES_SHARDED
 
     def pack_and_logits(self):
         s, _lib, F = self.s, self._lib, self.s["F"]
@@ -157,52 +158,69 @@ class Layer:
                       s["bias"].data_ptr(), 0.2, self.st.data_ptr(), self.xmax.data_ptr(),
                       self.out.data_ptr(), None, self.stream)
             return
-        # a shard: [s | t] and the lone outputs of the own destinations in one
-        # pass; the other rows' s from the all-gather (N > 1) or, for the tests'
-        # virtual shards on one GPU, from a logits pass over every row
+        # a shard: s | t and the lone outputs of the own destinations in one
+        # pass, s straight into the rank's block of s_all.  The tests' virtual
+        # shards on one GPU (world 1) take the other rows' s from a logits pass
+        # over every row (the all-gather's stand-in, untimed by bench)
         n = self.n_dst
         if self.world == 1:
             _lib.call("gfd_gat_logits_ex", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
                       self.packed.data_ptr(), H, C, self.st.data_ptr(), self.xmax.data_ptr(),
                       self.stream)
+            self.s_all.copy_(self.st[:, :H])
         if n > 0:
-            _lib.call("gfd_gat_logits_lone", x[spec.dst_lo:].data_ptr(), self.xdt, n, F,
+            _lib.call("gfd_gat_logits_lone_split", x[spec.dst_lo:].data_ptr(), self.xdt, n, F,
                       s["ldx"], self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
-                      s["bias"].data_ptr(), 0.2, self.st_local.data_ptr(), self.xmax.data_ptr(),
-                      self.out.data_ptr(), None, self.stream)
-        if self.world > 1:
-            import torch.distributed as dist
-            if n > 0:
-                self.s_local[:n] = self.st_local[:n, :H]
-            dist.all_gather_into_tensor(self.s_all, self.s_local)
-            for r in range(self.world):
-                lo, sz = spec.dst_bounds[r], self.sizes[r]
-                self.st[lo:lo + sz, :H] = self.s_all[r * self.per:r * self.per + sz]
-            dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
-        if n > 0:
-            self.st[spec.dst_lo:spec.dst_hi] = self.st_local[:n]
+                      s["bias"].data_ptr(), 0.2, self.s_all[spec.dst_lo:].data_ptr(), H,
+                      self.t_loc.data_ptr(), H, self.xmax.data_ptr(), self.out.data_ptr(), None,
+                      self.stream)
+
+    def exchange(self):
+        # ONE all-gather-v of the [N, 8] source logits (RCCL; uneven blocks land
+        # at their node rows) and the max |x| reduction the tile stage's row
+        # scale needs
+        import torch.distributed as dist
+        r = self.s["spec"].rank
+        if all(b.shape == self.s_blocks[0].shape for b in self.s_blocks):
+            # equal blocks: s_all IS the gathered layout (in place, no copy-out)
+            dist.all_gather_into_tensor(self.s_all, self.s_blocks[r])
+        else:  # uneven blocks (RCCL grouped broadcasts into the row views)
+            dist.all_gather(self.s_blocks, self.s_blocks[r])
+        dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
 
     def aggregate(self, stages):
         s = self.s
-        self._lib.call("gfd_gat_aggregate_ex", s["x"].data_ptr(), self.xdt, self.N, s["F"],
+        if self.whole:
+            self._lib.call("gfd_gat_aggregate_ex", s["x"].data_ptr(), self.xdt, self.N, s["F"],
+                           s["ldx"], s["shard"].rowptr.data_ptr(), s["graph"].col.data_ptr(),
+                           self.n_dst, 0, self.st.data_ptr(), self.xmax.data_ptr(),
+                           self.packed.data_ptr(), s["bias"].data_ptr(), H, C, 0.2, 0.0, 0,
+                           self.cplan, stages, self.out.data_ptr(), None, self.ws.data_ptr(),
+                           self.ws.numel(), self.stream)
+            return
+        self._lib.call("gfd_gat_aggregate_split", s["x"].data_ptr(), self.xdt, self.N, s["F"],
                        s["ldx"], s["shard"].rowptr.data_ptr(), s["graph"].col.data_ptr(),
-                       self.n_dst, s["spec"].dst_lo, self.st.data_ptr(), self.xmax.data_ptr(),
-                       self.packed.data_ptr(), s["bias"].data_ptr(), H, C, 0.2, 0.0, 0,
-                       self.cplan, stages, self.out.data_ptr(), None, self.ws.data_ptr(),
-                       self.ws.numel(), self.stream)
+                       self.n_dst, s["spec"].dst_lo, self.s_all.data_ptr(), H,
+                       self.t_loc.data_ptr(), H, self.xmax.data_ptr(), self.packed.data_ptr(),
+                       s["bias"].data_ptr(), H, C, 0.2, 0.0, 0, self.cplan, stages, None,
+                       self.out.data_ptr(), None, self.ws.data_ptr(), self.ws.numel(),
+                       self.stream)
 
-    STAGES = (("pack+logits", None), ("hubs", STAGE_HUBS), ("general", STAGE_MID),
-              ("light", STAGE_LIGHT), ("lone", STAGE_LONE))
     STAGES_FUSED = (("pack+logits+lone", None), ("hubs", STAGE_HUBS), ("general", STAGE_MID),
                     ("light", STAGE_LIGHT))
+    STAGES_SHARDED = (("pack+logits+lone", None), ("exchange", "x"), ("hubs", STAGE_HUBS),
+                      ("general", STAGE_MID), ("light", STAGE_LIGHT))
 
     def step(self, evs=None):
-        # events record on torch's current stream == the stream every gfd launch uses
+        # events record on torch's current stream == the stream every gfd launch
+        # uses (and the one RCCL's collectives are ordered against)
         for k, (_, stg) in enumerate(self.stages):
             if evs:
                 evs[k].record()
             if stg is None:
                 self.pack_and_logits()
+            elif stg == "x":
+                self.exchange()
             else:
                 self.aggregate(stg)
         if evs:
@@ -230,11 +248,12 @@ def time_layer(layer, steps, warmup, world):
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
     stage_ms = {name: med([e[k].elapsed_time(e[k + 1]) for e in events])
                 for k, (name, _) in enumerate(layer.stages)}
+    mine = elapsed
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=layer.dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    return elapsed, stage_ms
+    return elapsed, stage_ms, mine
 
 
 def stage_bytes(s, plan, esz):
@@ -261,10 +280,12 @@ def stage_bytes(s, plan, esz):
     W_b = 4 * F * H * C
     hub_msgs = int(sdeg[hubs_mask].sum().item())
     out_b = 4 + 4 * C
+    n_rows = s["spec"].dst_hi - s["spec"].dst_lo   # rows the rank's logits pass streams
     res = {
-        "pack+logits": s["graph"].num_nodes * (F * esz + 64) + W_b,
-        "pack+logits+lone": s["graph"].num_nodes * (F * esz + 64 + 4) + W_b +
-                            int(lone.sum().item()) * out_b,
+        "pack+logits": n_rows * (F * esz + 64) + W_b,
+        "pack+logits+lone": n_rows * (F * esz + 64 + 4) + W_b + int(lone.sum().item()) * out_b,
+        # the all-gathered source logits land in HBM once: 32 B per node
+        "exchange": s["graph"].num_nodes * H * 4,
         "hubs": hub_msgs * row_b + plan.num_chunks * 4 * (16 + 8 * ((F + 7) // 8 * 8)),
         "general": int(sdeg[gen & ~hubs_mask].sum().item()) * row_b +
                    int(gen.sum().item()) * out_b + W_b,
@@ -357,22 +378,24 @@ def measure(args, dev, rank, world, config):
         f"setup {time.perf_counter() - t_setup:.1f}s")
     if getattr(args, "legs_only", False) and config == "c4":
         return {"legs_only": True}, s, layer
-    elapsed, stage_ms = time_layer(layer, args.steps, args.warmup, world)
+    elapsed, stage_ms, rank_elapsed = time_layer(layer, args.steps, args.warmup, world)
     ms_step = elapsed * 1e3 / args.steps
     value = E * args.steps / elapsed
     M = s["graph"].num_messages
     B_layer = M * (esz * F + 4) + N * (4 + 4 * C) + 4 * F * H * C
     flop_layer = 2 * N * F * H * C + M * H * (2 * C + 8)
-    t_roof = max(B_layer / (HBM_PEAK_GBPS * 1e9), flop_layer / (BF16_PEAK_TFLOPS * 1e12))
+    # per GPU: the layer's bytes and flops split over the ranks (dst sharding)
+    t_roof = max(B_layer / (HBM_PEAK_GBPS * 1e9), flop_layer / (BF16_PEAK_TFLOPS * 1e12)) / world
     sb, counts = stage_bytes(s, plan, esz)
     kernels = {}
     for name, ms in stage_ms.items():
         gbps = sb[name] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         kernels[name] = {"ms": ms, "algorithmic_bytes": sb[name], "gbps": gbps,
                          "frac": gbps / HBM_PEAK_GBPS}
-    dom = max(kernels, key=lambda k: kernels[k]["ms"])
+    dom = max((k for k in kernels if k != "exchange"), key=lambda k: kernels[k]["ms"])
     kname = {"pack+logits": "k_logits_s (+ pack)",
              "pack+logits+lone": "k_logits_lone (+ pack): logits + self-loop-only rows",
+             "exchange": "RCCL all-gather-v of the [N, 8] source logits + max|x| all-reduce",
              "hubs": "k_hub_partial + k_hub_fin",
              "general": "k_stream<general> (hub rows, 7+ messages)",
              "light": "k_stream<light> (2-6 messages)",
@@ -403,17 +426,71 @@ def measure(args, dev, rank, world, config):
         "kernels": kernels,
         "layer": {"algorithmic_bytes": B_layer, "flop": flop_layer,
                   "hbm_gbps": B_layer / (ms_step * 1e-3) / 1e9,
+                  "hbm_gbps_per_gpu": B_layer / world / (ms_step * 1e-3) / 1e9,
                   "t_roof_ms": t_roof * 1e3, "roofline_frac": t_roof / (ms_step * 1e-3)},
         "cpu_baseline": None,
     }
+    if world > 1:
+        # every rank's own clock and stages (rank 0 prints them): the line's
+        # ms_per_step is the max over ranks
+        import torch.distributed as dist
+        mine = {"rank": rank, "elapsed_s": rank_elapsed, "stage_ms": stage_ms,
+                "dst": [s["spec"].dst_lo, s["spec"].dst_hi],
+                "messages": int(s["shard"].rowptr[-1].item() - s["shard"].rowptr[0].item()),
+                "device": torch.cuda.get_device_name(dev)}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        res["distributed"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                              "ranks": allr}
     return res, s, layer
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_command(args, argv, port: int):
+    """The command that runs ``--gpus N`` as N ranks: torch.distributed.run
+    with one process per GPU on this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+            f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(args, argv, device_count=None, run=None) -> int:
+    """``python bench.py --gpus N`` (N > 1) outside a launcher: start the N
+    ranks as a CHILD torch.distributed.run and return its exit status.  This
+    process never touches the GPU (device_count() only counts devices on this
+    image; no HIP context is created) and never re-execs itself.  Fewer than N
+    visible devices is an error (exit 2), not a silently smaller run."""
+    import subprocess
+    n = args.gpus
+    have = torch.cuda.device_count() if device_count is None else device_count
+    if have < n:
+        log(f"[bench] --gpus {n}: only {have} device(s) visible; refusing to time fewer ranks")
+        return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL peer buffers)
+    cmd = rank_command(args, argv, free_port())
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    return (run or subprocess.call)(cmd, env=env)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is None:
+        args.gpus = world
+    if world != args.gpus:
+        log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing a mismatched run")
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)

@@ -33,9 +33,10 @@ __device__ __forceinline__ void mfma_step_split(const _Float16* __restrict__ zh,
 template <typename XT, int KF, int OCC>
 __global__ void __launch_bounds__(1024, OCC) k_fused(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ rowptr,
-    const int32_t* __restrict__ col, int64_t num_dst, int64_t dst_offset,
+    const int32_t* __restrict__ col, int64_t num_dst,
     const int32_t* __restrict__ order, const int4* __restrict__ desc,
-    const float* __restrict__ st, const PackHeader* __restrict__ hdr,
+    const float* __restrict__ s, int lds, const float* __restrict__ t, int ldt,
+    const PackHeader* __restrict__ hdr,
     const uint4* __restrict__ whi, const uint4* __restrict__ wlo, const float* __restrict__ bias,
     float slope, float dp, uint64_t seed, const int32_t* __restrict__ hub_rank,
     const float* __restrict__ zhub, float* __restrict__ out, float* __restrict__ stats,
@@ -80,8 +81,8 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
         }
     } else {
       const int e0 = dsc.y, e1 = dsc.z;
-      const float t_h = st[(dst_offset + i) * 16 + H + (lane & 7)];
-      SegState S = aggregate_segment<XT, KF>(x, ldx, F, col, e0, e1, st, t_h, slope, dp, seed, z);
+      const float t_h = lrow(t, int(i), ldt)[lane & 7];
+      SegState S = aggregate_segment<XT, KF>(x, ldx, F, col, e0, e1, s, lds, t_h, slope, dp, seed, z);
       const float inv_lane = 1.0f / (S.ssum + kSoftmaxEps);
       if (stats && lane < 8) {
         stats[i * 16 + lane] = S.m;
@@ -202,8 +203,8 @@ gfd_status launch_fused_t(const AggArgs& a, const PackLayout& L, hipStream_t str
   const int64_t tiles = (a.num_dst + kTile - 1) / kTile;
   auto kern = KF >= 2 ? &k_fused<XT, KF, 4> : &k_fused<XT, KF, 8>;
   kern<<<int(tiles), kFusedWaves * 64, fused_smem(L.Fp), stream>>>(
-      a.x, a.F, L.Fp, a.ldx, a.rowptr, a.col, a.num_dst, a.dst_offset, p.row_order,
-      reinterpret_cast<const int4*>(p.slot_desc), a.st,
+      a.x, a.F, L.Fp, a.ldx, a.rowptr, a.col, a.num_dst, p.row_order,
+      reinterpret_cast<const int4*>(p.slot_desc), a.s, a.lds, a.t, a.ldt,
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.whi_off),
       reinterpret_cast<const uint4*>(a.packed + L.wlo_off), a.bias, a.slope, a.dp, a.seed,

@@ -352,11 +352,20 @@ struct SegState {
   float ssum;
 };
 
+// Logits rows: the source logits s live in [N, lds] (columns 0..H-1, global
+// node rows), the destination logits t in [num_dst, ldt] (local destination
+// rows).  [N, 16] st tables are s = st, t = st + 16 dst_offset + H, both
+// strides 16; the sharded exchange gathers s as [N, 8] rows.  One unsigned
+// 32 x 32 -> 64-bit product per row (v_mad_u64_u32), as xrow.
+__device__ __forceinline__ const float* lrow(const float* p, int r, int ld) {
+  return p + uint64_t(uint32_t(r)) * uint64_t(uint32_t(ld));
+}
+
 template <typename XT, int KF>
 __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x, int64_t ldx,
                                                       int F, const int32_t* __restrict__ col,
-                                                      int e0, int e1, const float* __restrict__ st,
-                                                      float t_h, float slope, float dp,
+                                                      int e0, int e1, const float* __restrict__ s,
+                                                      int lds, float t_h, float slope, float dp,
                                                       uint64_t seed, float (&acc)[H][KF]) {
   const int lane = threadIdx.x & 63;
   const int h = lane & 7, kk = lane >> 3;
@@ -381,7 +390,7 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
       cn = col[min(b + 64 + lane, e1 - 1)];
     }
     const int j = __builtin_amdgcn_ds_bpermute((b - wb + kk) << 2, cw);
-    sv = st[int64_t(j) * 16 + h];
+    sv = lrow(s, j, lds)[h];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       // plain loads, f >= F reads x[F - 1] and selects 0: never the row padding
@@ -470,7 +479,9 @@ struct AggArgs {
   const void* x; int xdt; int F; int64_t ldx;
   int64_t N;
   const int32_t* rowptr; const int32_t* col; int64_t num_dst; int64_t dst_offset;
-  const float* st; const char* packed; const float* bias; float slope; float dp; uint64_t seed;
+  const float* s; int lds;  // source logits [N, lds] (lrow)
+  const float* t; int ldt;  // destination logits [num_dst, ldt], local rows
+  const char* packed; const float* bias; float slope; float dp; uint64_t seed;
   gfd_plan plan; int stages; float* out; float* stats;
   float* part; float* zhub;
   const float* xmax;  // max |x| over all rows of x (nullable): one scale for every Z row
@@ -493,8 +504,9 @@ gfd_status launch_logits(const void* x, int xdt, int64_t rows, int F, int64_t ld
 bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx);
 gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
                               const PackLayout& L, const char* packed, const int32_t* rowptr,
-                              const float* bias, float slope, float* st, float* xmax, float* out,
-                              float* stats, const Epi& ep, hipStream_t stream);
+                              const float* bias, float slope, float* s, int lds, float* t,
+                              int ldt, float* xmax, float* out, float* stats, const Epi& ep,
+                              hipStream_t stream);
 
 inline int kf_for(int F) { return (F + 63) / 64; }
 

@@ -169,20 +169,23 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int F, int
   return s.off;
 }
 
-gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
-                                const int32_t* rowptr, const int32_t* col, int64_t num_dst,
-                                int64_t dst_offset, const float* st, const float* xmax,
-                                const void* packed, const float* bias, int heads, int channels,
-                                float slope, float dp, uint64_t seed, const gfd_plan* plan,
-                                int stages, const gfd_epilogue* ep, float* out, float* stats,
-                                void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+                                   const int32_t* rowptr, const int32_t* col, int64_t num_dst,
+                                   int64_t dst_offset, const float* s_log, int64_t s_stride,
+                                   const float* t_log, int64_t t_stride, const float* xmax,
+                                   const void* packed, const float* bias, int heads, int channels,
+                                   float slope, float dp, uint64_t seed, const gfd_plan* plan,
+                                   int stages, const gfd_epilogue* ep, float* out, float* stats,
+                                   void* ws, size_t ws_bytes, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   const gfd_plan p = plan_or_empty(plan);
   gfd_status s =
       check_agg_args(x, x_dtype, N, F, ldx, rowptr, col, num_dst, dst_offset, dp, p, out);
   if (s != GFD_OK) return s;
-  if (!st || !packed || stages < 1 || stages > 31) return GFD_ERR_ARGUMENT;
+  if (!s_log || !t_log || !packed || stages < 1 || stages > 31) return GFD_ERR_ARGUMENT;
+  if (s_stride < H || t_stride < H || s_stride > (1 << 20) || t_stride > (1 << 20))
+    return GFD_ERR_ARGUMENT;
   Epi e{nullptr, 0, nullptr, 0};
   if (ep) {  // inference epilogue (see gfd_gat_fwd_ep); residual rows indexed like out
     if (!ep->scale_shift || stats || dp > 0.f) return GFD_ERR_ARGUMENT;
@@ -193,13 +196,29 @@ gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t N, int F, in
   const PackLayout L = pack_layout(F);
   s = check_graph(rowptr, col, num_dst, N, plan, nullptr, nullptr, nullptr, 0, stream);
   if (s != GFD_OK) return s;
-  AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, num_dst, dst_offset, st,
-            static_cast<const char*>(packed), bias, slope, dp, seed, p, stages, out, stats,
-            nullptr, nullptr, xmax, e};
+  AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, num_dst, dst_offset, s_log, int(s_stride),
+            t_log, int(t_stride), static_cast<const char*>(packed), bias, slope, dp, seed, p,
+            stages, out, stats, nullptr, nullptr, xmax, e};
   Carve c(ws, ws_bytes);
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.zhub);
   if (!c.ok && p.num_hubs > 0) return GFD_ERR_WORKSPACE;
   return aggregate_impl(a, stream);
+}
+
+gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+                                const int32_t* rowptr, const int32_t* col, int64_t num_dst,
+                                int64_t dst_offset, const float* st, const float* xmax,
+                                const void* packed, const float* bias, int heads, int channels,
+                                float slope, float dp, uint64_t seed, const gfd_plan* plan,
+                                int stages, const gfd_epilogue* ep, float* out, float* stats,
+                                void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+  // [N, 16] table: s = columns 0..7 of every row, t = columns 8..15 of the
+  // destination range's rows
+  if (!st || dst_offset < 0) return GFD_ERR_ARGUMENT;
+  return gfd_gat_aggregate_split(x, x_dtype, N, F, ldx, rowptr, col, num_dst, dst_offset, st, 16,
+                                 st + dst_offset * 16 + H, 16, xmax, packed, bias, heads,
+                                 channels, slope, dp, seed, plan, stages, ep, out, stats, ws,
+                                 ws_bytes, stream_);
 }
 
 gfd_status gfd_gat_aggregate_ex(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
@@ -247,15 +266,16 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
     return GFD_ERR_WORKSPACE;
   const PackLayout L = pack_layout(F);
   Carve c(ws, ws_bytes);
-  AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, N, 0, st, nullptr, bias, slope, dp, seed, p,
-            GFD_STAGE_ALL, out, stats, nullptr, nullptr, nullptr, e};
+  AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, N, 0, st, 16, st ? st + H : nullptr, 16, nullptr,
+            bias, slope, dp, seed, p, GFD_STAGE_ALL, out, stats, nullptr, nullptr, nullptr, e};
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.zhub);
   void* packed = c.take<char>(L.bytes);
   float* st_ws = c.take<float>(size_t(N) * 16);
   float* xmax = c.take<float>(1);
   if (!c.ok) return GFD_ERR_WORKSPACE;
   if (st == nullptr) st = st_ws;
-  a.st = st;
+  a.s = st;
+  a.t = st + H;
   a.packed = static_cast<const char*>(packed);
   a.xmax = xmax;
   s = check_graph(rowptr, col, N, N, plan, nullptr, nullptr, nullptr, 0, stream);
@@ -266,8 +286,8 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
   if (lone_fusable(a, L)) {
     // the lone destinations' outputs come out of the logits pass; the tile
     // stage runs the general and light classes only
-    s = launch_logits_lone(x, x_dtype, N, F, ldx, L, a.packed, rowptr, bias, slope, st, xmax,
-                           out, stats, a.ep, stream);
+    s = launch_logits_lone(x, x_dtype, N, F, ldx, L, a.packed, rowptr, bias, slope, st, 16,
+                           st + H, 16, xmax, out, stats, a.ep, stream);
     if (s != GFD_OK) return s;
     a.stages = GFD_STAGE_HUBS | GFD_STAGE_TILES_GENERAL | GFD_STAGE_TILES_LIGHT;
   } else {

@@ -18,16 +18,16 @@ namespace {
 template <typename XT, int KF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_hub_partial(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
-    int64_t dst_offset, const float* __restrict__ st, float slope, float dp, uint64_t seed,
+    const float* __restrict__ s, int lds, const float* __restrict__ t, int ldt, float slope, float dp, uint64_t seed,
     const int4* __restrict__ chunks, int64_t num_chunks, float* __restrict__ part) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (blockIdx.x * int64_t(blockDim.x) + threadIdx.x) >> 6;
   if (c >= num_chunks) return;
   const int4 ck = chunks[c];
-  const float t_h = st[(dst_offset + ck.w) * 16 + H + (lane & 7)];
+  const float t_h = lrow(t, ck.w, ldt)[lane & 7];
   float acc[H][KF];
   SegState S =
-      aggregate_segment<XT, KF>(x, ldx, F, col, ck.y, ck.z, st, t_h, slope, dp, seed, acc);
+      aggregate_segment<XT, KF>(x, ldx, F, col, ck.y, ck.z, s, lds, t_h, slope, dp, seed, acc);
   const int KP = H * Fp;
   float* pr = part + c * (16 + KP);
   if (lane < 8) {
@@ -113,7 +113,7 @@ gfd_status launch_hubs_t(const AggArgs& a, const PackLayout& L, hipStream_t stre
   const gfd_plan& p = a.plan;
   const int64_t blocks = (p.num_chunks + 3) / 4;
   k_hub_partial<XT, KF><<<int(blocks), 256, 0, stream>>>(
-      a.x, a.F, L.Fp, a.ldx, a.col, a.dst_offset, a.st, a.slope, a.dp, a.seed,
+      a.x, a.F, L.Fp, a.ldx, a.col, a.s, a.lds, a.t, a.ldt, a.slope, a.dp, a.seed,
       reinterpret_cast<const int4*>(p.hub_chunk), p.num_chunks, a.part);
   GFD_LAUNCH_CHECK();
   const int slices = (L.KP / 4 + 63) / 64;

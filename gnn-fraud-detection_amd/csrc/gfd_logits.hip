@@ -44,7 +44,8 @@ k_logits_lone(
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ uph,
     const uint4* __restrict__ upl, const uint4* __restrict__ wph, const uint4* __restrict__ wpl,
     const int32_t* __restrict__ rowptr, const float* __restrict__ bias, float slope,
-    float* __restrict__ st, float* __restrict__ xmax, float* __restrict__ out,
+    float* __restrict__ sl, int lds, float* __restrict__ tl, int ldt, float* __restrict__ xmax,
+    float* __restrict__ out,
     float* __restrict__ stats, Epi ep) {
   __shared__ uint4 WB[2][kLKB][4][64];  // permuted Wbar hi / lo fragments, zero past KB
   __shared__ uint4 UP[2][kLKB][64];     // permuted [U | V] hi / lo fragments, zero past KB
@@ -180,7 +181,8 @@ k_logits_lone(
       const float eq = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers)));
       sv[q] = acc[q] * (eq * uvu);
       const int64_t orow = t * 16 + src;
-      if (orow < rows) st[orow * 16 + rl] = sv[q];
+      // s | t columns of the row (sl / tl: separate tables, any strides)
+      if (orow < rows) (rl < H ? sl + uint64_t(orow) * lds : tl + uint64_t(orow) * ldt - H)[rl] = sv[q];
     }
     if (!any_lone) continue;
     const int lone_i = lone ? 1 : 0;
@@ -215,8 +217,8 @@ k_logits_lone(
 template <typename XT>
 gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackLayout& L,
                     const char* packed, const int32_t* rowptr, const float* bias, float slope,
-                    float* st, float* xmax, float* out, float* stats, const Epi& ep,
-                    hipStream_t stream) {
+                    float* s, int lds, float* t, int ldt, float* xmax, float* out,
+                    float* stats, const Epi& ep, hipStream_t stream) {
   const int64_t tiles = (rows + 15) / 16;
   int64_t nb = (tiles + kLLWaves - 1) / kLLWaves;
   const int64_t cap = int64_t(cu_count()) * 2;  // resident blocks; grid-stride beyond
@@ -229,8 +231,8 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
       reinterpret_cast<const uint4*>(packed + (plain ? L.ush_off : L.uph_off)),
       reinterpret_cast<const uint4*>(packed + (plain ? L.usl_off : L.upl_off)),
       reinterpret_cast<const uint4*>(packed + (plain ? L.wbh_off : L.wph_off)),
-      reinterpret_cast<const uint4*>(packed + (plain ? L.wbl_off : L.wpl_off)), rowptr, bias, slope, st, xmax, out,
-      stats, ep);
+      reinterpret_cast<const uint4*>(packed + (plain ? L.wbl_off : L.wpl_off)), rowptr, bias, slope, s, lds, t, ldt,
+      xmax, out, stats, ep);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
@@ -249,15 +251,16 @@ bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx) {
 
 gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,
                               const PackLayout& L, const char* packed, const int32_t* rowptr,
-                              const float* bias, float slope, float* st, float* xmax, float* out,
-                              float* stats, const Epi& ep, hipStream_t stream) {
+                              const float* bias, float slope, float* s, int lds, float* t,
+                              int ldt, float* xmax, float* out, float* stats, const Epi& ep,
+                              hipStream_t stream) {
   if (rows <= 0) return GFD_OK;
   if (!logits_lone_supported(x, xdt, F, ldx)) return GFD_ERR_UNSUPPORTED;
   return xdt == GFD_DTYPE_BF16
-             ? launch_t<XBF16>(x, rows, F, ldx, L, packed, rowptr, bias, slope, st, xmax, out,
-                               stats, ep, stream)
-             : launch_t<XF32>(x, rows, F, ldx, L, packed, rowptr, bias, slope, st, xmax, out,
-                              stats, ep, stream);
+             ? launch_t<XBF16>(x, rows, F, ldx, L, packed, rowptr, bias, slope, s, lds, t, ldt,
+                               xmax, out, stats, ep, stream)
+             : launch_t<XF32>(x, rows, F, ldx, L, packed, rowptr, bias, slope, s, lds, t, ldt,
+                              xmax, out, stats, ep, stream);
 }
 
 }  // namespace fwd
@@ -265,21 +268,35 @@ gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64
 
 extern "C" {
 
+gfd_status gfd_gat_logits_lone_split(const void* x, int x_dtype, int64_t num_nodes,
+                                     int in_features, int64_t x_stride, const void* packed,
+                                     int heads, int channels, const int32_t* rowptr,
+                                     const float* bias, float negative_slope, float* s,
+                                     int64_t s_stride, float* t, int64_t t_stride, float* xmax,
+                                     float* out, float* stats, gfd_stream_t stream_) {
+  if (heads != H || channels != C || in_features < 1 || in_features > 256)
+    return GFD_ERR_UNSUPPORTED;
+  if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
+  if (num_nodes < 0 || x_stride < in_features) return GFD_ERR_ARGUMENT;
+  if (s_stride < H || t_stride < H || s_stride > (1 << 20) || t_stride > (1 << 20))
+    return GFD_ERR_ARGUMENT;
+  if (num_nodes > 0 && (!x || !packed || !rowptr || !s || !t || !out)) return GFD_ERR_ARGUMENT;
+  const PackLayout L = pack_layout(in_features);
+  return launch_logits_lone(x, x_dtype, num_nodes, in_features, x_stride, L,
+                            static_cast<const char*>(packed), rowptr, bias, negative_slope, s,
+                            int(s_stride), t, int(t_stride), xmax, out, stats,
+                            Epi{nullptr, 0, nullptr, 0}, static_cast<hipStream_t>(stream_));
+}
+
 gfd_status gfd_gat_logits_lone(const void* x, int x_dtype, int64_t num_nodes, int in_features,
                                int64_t x_stride, const void* packed, int heads, int channels,
                                const int32_t* rowptr, const float* bias, float negative_slope,
                                float* st, float* xmax, float* out, float* stats,
                                gfd_stream_t stream_) {
-  if (heads != H || channels != C || in_features < 1 || in_features > 256)
-    return GFD_ERR_UNSUPPORTED;
-  if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
-  if (num_nodes < 0 || x_stride < in_features) return GFD_ERR_ARGUMENT;
-  if (num_nodes > 0 && (!x || !packed || !rowptr || !st || !out)) return GFD_ERR_ARGUMENT;
-  const PackLayout L = pack_layout(in_features);
-  return launch_logits_lone(x, x_dtype, num_nodes, in_features, x_stride, L,
-                            static_cast<const char*>(packed), rowptr, bias, negative_slope, st,
-                            xmax, out, stats, Epi{nullptr, 0, nullptr, 0},
-                            static_cast<hipStream_t>(stream_));
+  if (num_nodes > 0 && !st) return GFD_ERR_ARGUMENT;
+  return gfd_gat_logits_lone_split(x, x_dtype, num_nodes, in_features, x_stride, packed, heads,
+                                   channels, rowptr, bias, negative_slope, st, 16,
+                                   st ? st + H : nullptr, 16, xmax, out, stats, stream_);
 }
 
 }  // extern "C"

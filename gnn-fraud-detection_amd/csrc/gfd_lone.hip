@@ -49,7 +49,8 @@ __device__ __forceinline__ void load8(const typename XT::T* __restrict__ r, int 
 template <typename XT, int KB>
 __global__ void __launch_bounds__(kLWaves * 64) k_lone(
     const typename XT::T* __restrict__ x, int F, int64_t ldx, int64_t num_dst,
-    int64_t dst_offset, const int4* __restrict__ desc, const float* __restrict__ st,
+    int64_t dst_offset, const int4* __restrict__ desc, const float* __restrict__ s, int lds,
+    const float* __restrict__ t, int ldt,
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ wbh,
     const uint4* __restrict__ wbl, const float* __restrict__ bias, float slope,
     float* __restrict__ out, float* __restrict__ stats, const int64_t* __restrict__ split,
@@ -129,8 +130,8 @@ __global__ void __launch_bounds__(kLWaves * 64) k_lone(
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int h = g + 4 * k;
-        const float* sr = st + (dst_offset + row) * 16;
-        stats[int64_t(row) * 16 + h] = leaky(sr[h] + sr[H + h], slope);
+        const float sv = lrow(s, int(dst_offset + row), lds)[h];
+        stats[int64_t(row) * 16 + h] = leaky(sv + lrow(t, row, ldt)[h], slope);
         stats[int64_t(row) * 16 + H + h] = 1.0f;
       }
     }
@@ -147,7 +148,7 @@ gfd_status launch_lone_k(const AggArgs& a, const PackLayout& L, hipStream_t stre
   const gfd_plan& p = a.plan;
   k_lone<XT, KB><<<int(grid), kLWaves * 64, 0, stream>>>(
       static_cast<const typename XT::T*>(a.x), a.F, a.ldx, a.num_dst, a.dst_offset,
-      reinterpret_cast<const int4*>(p.slot_desc), a.st,
+      reinterpret_cast<const int4*>(p.slot_desc), a.s, a.lds, a.t, a.ldt,
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wbh_off),
       reinterpret_cast<const uint4*>(a.packed + L.wbl_off), a.bias, a.slope, a.out, a.stats,

@@ -113,7 +113,8 @@ template <int PART, typename XT, int KF, bool LIGHT, int NRW>
 __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW>& q,
                                               const void* __restrict__ x, int64_t ldx, int F,
                                               const int32_t* __restrict__ col,
-                                              const float* __restrict__ st, int64_t dst_offset,
+                                              const float* __restrict__ s, int lds,
+                                              const float* __restrict__ t, int ldt,
                                               SlotRing* __restrict__ ring, int lane) {
   if constexpr (PART == 0) {
     const int h = lane & 7;
@@ -122,8 +123,8 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW
     const int e1 = __builtin_amdgcn_readlane(p.v, 2);
     const int hw = __builtin_amdgcn_readlane(p.v, 3);
     const int jm = __builtin_amdgcn_ds_bpermute((8 + (lane >> 3)) << 2, p.v);  // message lane >> 3
-    q.th = st[(dst_offset + row) * 16 + H + h];
-    q.sj = st[int64_t(jm) * 16 + h];
+    q.th = lrow(t, row, ldt)[h];
+    q.sj = lrow(s, jm, lds)[h];
     if constexpr (!LIGHT) {
       // sources of messages 8 .. 71 (one per lane), range-checked: light, hub
       // and empty slots fetch nothing
@@ -228,7 +229,7 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
                                            const SlotRows<KF>& q, const void* __restrict__ x,
                                            int64_t ldx, int F, int Fp,
                                            const int32_t* __restrict__ col,
-                                           const float* __restrict__ st, float slope, float dp,
+                                           const float* __restrict__ s, int lds, float slope, float dp,
                                            uint64_t seed, const float* __restrict__ zhub,
                                            float* __restrict__ stats, _Float16* __restrict__ zh,
                                            _Float16* __restrict__ zl, float* __restrict__ rsc,
@@ -284,7 +285,7 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
         cb = b;
       }
       const int jl = __builtin_amdgcn_ds_bpermute((b - cb + kk) << 2, cj);
-      sv = st[int64_t(jl) * 16 + h];
+      sv = lrow(s, jl, lds)[h];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(cj, b - cb + k), ldx), F, lane,
@@ -344,9 +345,9 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
 template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
-    int64_t num_dst, int64_t dst_offset, const int4* __restrict__ desc,
-    const int32_t* __restrict__ cols8, const float* __restrict__ st,
-    const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
+    int64_t num_dst, const int4* __restrict__ desc,
+    const int32_t* __restrict__ cols8, const float* __restrict__ s, int lds,
+    const float* __restrict__ t, int ldt, const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
     const uint4* __restrict__ wsl, const float* __restrict__ bias, float slope, float dp,
     uint64_t seed, const float* __restrict__ zhub, float* __restrict__ out,
     float* __restrict__ stats, const float* __restrict__ xmax,
@@ -409,7 +410,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   sl_rec(n0, slot(0, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(0, r1), num_dst, lim, desc, cols8, lane);
 #define GFD_ISSUE(P, n, d, ring) \
-  sl_issue_part<P, XT, KF, LIGHT>(n, d, x, ldx, F, col, st, dst_offset, ring, lane)
+  sl_issue_part<P, XT, KF, LIGHT>(n, d, x, ldx, F, col, s, lds, t, ldt, ring, lane)
   GFD_ISSUE(0, n0, d0, ring0 + r0); GFD_ISSUE(1, n0, d0, ring0 + r0);
   GFD_ISSUE(2, n0, d0, ring0 + r0); GFD_ISSUE(3, n0, d0, ring0 + r0);
   GFD_ISSUE(4, n0, d0, ring0 + r0);
@@ -436,9 +437,9 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       sl_light<KF>(db, d1, kmax, slope, dp, seed, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid,
                    r1, erg, lane);
     } else {
-      sl_general<XT, KF>(rg + r0, d0, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+      sl_general<XT, KF>(rg + r0, d0, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub, stats,
                          Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane);
-      sl_general<XT, KF>(rg + r1, d1, x, ldx, F, Fp, col, st, slope, dp, seed, zhub, stats,
+      sl_general<XT, KF>(rg + r1, d1, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub, stats,
                          Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg, lane);
     }
   };
@@ -596,8 +597,8 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
   // general: the slots before the light class (every tile without a class split)
   const int64_t* split = p.class_split;
   kern<<<int(grid), kSWaves * 64, lds, stream>>>(
-      a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst, a.dst_offset,
-      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.st,
+      a.x, a.F, L.Fp, a.ldx, a.col, a.num_dst,
+      reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.s, a.lds, a.t, a.ldt,
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsl_off), a.bias, a.slope, a.dp, a.seed,

@@ -48,7 +48,7 @@ def test_ctypes_table_matches_header(lib):
 
 
 def test_version_and_status_strings(lib):
-    assert lib.gfd_abi_version() == 3
+    assert lib.gfd_abi_version() == 4
     assert b"range" in lib.gfd_status_string(2)
     assert lib.gfd_status_string(99) == b"unknown status"
 

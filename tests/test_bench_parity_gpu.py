@@ -124,17 +124,27 @@ def test_bench_multi_rank_path(world, monkeypatch):
     torch.cuda.synchronize()
     ref, st_full, xmax = whole.out.clone(), whole.st.clone(), whole.xmax.clone()
     bounds = gdist.edge_balanced_bounds(g.rowptr, world)
-    per = max(max(bounds[r + 1] - bounds[r] for r in range(world)), 1)
+    sent = []
 
-    def all_gather(out, inp, group=None):
-        assert out.shape == (per * world, H) and inp.shape == (per, H)
+    def all_gather(outs, inp, group=None):
+        # the rank's own block is the input (in place): its rows must already
+        # hold the fused logits pass's s, the other blocks land at their rows
+        assert len(outs) == world
+        me = next(q for q in range(world) if outs[q].data_ptr() == inp.data_ptr())
+        assert torch.equal(inp, st_full[bounds[me]:bounds[me + 1], :H])
         for q in range(world):
-            out[q * per:q * per + bounds[q + 1] - bounds[q]] = st_full[bounds[q]:bounds[q + 1], :H]
+            assert outs[q].shape == (bounds[q + 1] - bounds[q], H) and outs[q].is_contiguous()
+            outs[q].copy_(st_full[bounds[q]:bounds[q + 1], :H])
+        sent.append(me)
+
+    def all_gather_into_tensor(out, inp, group=None):
+        raise AssertionError("edge-balanced blocks are uneven: the list form is expected")
 
     def all_reduce(t, op=None, group=None):
         t.copy_(torch.maximum(t, xmax))
 
-    monkeypatch.setattr(tdist, "all_gather_into_tensor", all_gather)
+    monkeypatch.setattr(tdist, "all_gather", all_gather)
+    monkeypatch.setattr(tdist, "all_gather_into_tensor", all_gather_into_tensor)
     monkeypatch.setattr(tdist, "all_reduce", all_reduce)
     for r in range(world):
         sr = dict(s)
@@ -144,8 +154,10 @@ def test_bench_multi_rank_path(world, monkeypatch):
         layer.step()
         torch.cuda.synchronize()
         lo, hi = sr["spec"].dst_lo, sr["spec"].dst_hi
-        # [s | t] of the own rows from the fused pass: bit-identical per-row arithmetic
-        assert torch.equal(layer.st[lo:hi], st_full[lo:hi]), f"rank {r}: own logits"
+        # s | t of the own rows from the fused pass: bit-identical per-row arithmetic
+        assert torch.equal(layer.s_all, st_full[:, :H]), f"rank {r}: gathered s table"
+        assert torch.equal(layer.t_loc[:hi - lo], st_full[lo:hi, H:]), f"rank {r}: own t"
+        assert sent[-1] == r
         assert_close(layer.out[:hi - lo], ref[lo:hi], atol=1e-5, rtol=1e-5,
                      what=f"rank {r} of {world}")
         del layer
