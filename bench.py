@@ -60,6 +60,13 @@ def parse(argv=None):
     p.add_argument("--gamma", type=float, default=2.1)
     p.add_argument("--row-align", type=int, default=16,
                    help="byte alignment of x rows (16: pitch 168; 128: whole cache lines)")
+    p.add_argument("--balance", choices=["nodes", "messages"], default="nodes",
+                   help="N > 1 destination shards: equal node blocks (C4's ids are randomly "
+                        "permuted: messages within 2.6 %% at 8 ranks) or message-balanced ranges")
+    p.add_argument("--rehearse", action="store_true",
+                   help="N > 1 ranks on however many GPUs are visible (rank -> GPU rank %% "
+                        "count), gloo host-staged exchange: exercises the launcher and the "
+                        "per-rank path on a 1-GPU box; NOT a scaling measurement")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-legs", action="store_true")
     p.add_argument("--legs", default="c4bwd,sample,c5,c1,c2,c3,temporal,ingest",
@@ -79,7 +86,7 @@ def glorot(shape, gen, device):
 
 
 def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, world=1,
-          row_align=16):
+          row_align=16, balance="nodes"):
     """The bench workload, built on the device exactly as timed: Chung-Lu
     graph (seed 1) -> CSR, x ~ N(0,1) (seed 0) at a 16-B row pitch, glorot W
     (seed 0), zero bias, this rank's destination shard and its cached plan.
@@ -101,7 +108,7 @@ def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, worl
     a_s = glorot((1, H, C), gen, dev).contiguous()
     a_d = glorot((1, H, C), gen, dev).contiguous()
     bias = torch.zeros(C, device=dev)
-    spec = gdist.ShardSpec(g.rowptr, rank, world)   # dst shard + logits node block
+    spec = gdist.ShardSpec(g.rowptr, rank, world, balance)   # the rank's destinations
     shard = g.shard(spec.dst_lo, spec.dst_hi)
     return {"graph": g, "x": x, "xbuf": xbuf, "ldx": ldx, "W": W, "a_s": a_s, "a_d": a_d,
             "bias": bias, "spec": spec, "shard": shard, "dtype": dtype, "F": F}
@@ -129,10 +136,15 @@ class Layer:
         # table the kernels read: no scatter between collective and kernels),
         # t of the own destinations in t_loc [n_dst, 8]
         self.st = torch.empty((self.N, 2 * H), dtype=torch.float32, device=dev)
-        self.s_all = torch.empty((self.N, H), dtype=torch.float32, device=dev)
-        self.t_loc = torch.empty((max(self.n_dst, 1), H), dtype=torch.float32, device=dev)
         b = spec.dst_bounds
-        self.s_blocks = [self.s_all[b[r]:b[r + 1]] for r in range(world)]
+        # equal blocks (node balance): rank r's rows r*per .. are its nodes, the
+        # table padded to world*per rows; uneven blocks: views at their rows
+        self.equal = all(b[r] == r * spec.per for r in range(world))
+        rows = world * spec.per if self.equal else self.N
+        self.s_all = torch.empty((max(rows, self.N), H), dtype=torch.float32, device=dev)
+        self.t_loc = torch.empty((max(self.n_dst, 1), H), dtype=torch.float32, device=dev)
+        self.s_blocks = ([self.s_all[r * spec.per:(r + 1) * spec.per] for r in range(world)]
+                         if self.equal else [self.s_all[b[r]:b[r + 1]] for r in range(world)])
         self.out = torch.empty((max(self.n_dst, 1), C), dtype=torch.float32, device=dev)
         self.ws = torch.empty(self.lib.gfd_gat_fwd_workspace_size(
             self.N, self.n_dst, F, H, C, self.plan.num_hubs, self.plan.num_chunks),
@@ -181,9 +193,21 @@ class Layer:
         # scale needs
         import torch.distributed as dist
         r = self.s["spec"].rank
-        if all(b.shape == self.s_blocks[0].shape for b in self.s_blocks):
-            # equal blocks: s_all IS the gathered layout (in place, no copy-out)
-            dist.all_gather_into_tensor(self.s_all, self.s_blocks[r])
+        if dist.get_backend() == "gloo":   # --rehearse: the same exchange, host-staged
+            if not self.equal:
+                raise RuntimeError("--rehearse supports the node-balanced (equal-block) exchange")
+            per = self.s_blocks[0].shape[0]
+            cpu = self.s_all[:len(self.s_blocks) * per].cpu()
+            dist.all_gather_into_tensor(cpu, cpu[r * per:(r + 1) * per].clone())
+            self.s_all[:len(self.s_blocks) * per].copy_(cpu)
+            xm = self.xmax.cpu()
+            dist.all_reduce(xm, op=dist.ReduceOp.MAX)
+            self.xmax.copy_(xm)
+            return
+        if self.equal:
+            # s_all IS the gathered layout: in place, one RCCL all-gather
+            dist.all_gather_into_tensor(self.s_all[:len(self.s_blocks) * self.s_blocks[0].shape[0]],
+                                        self.s_blocks[r])
         else:  # uneven blocks (RCCL grouped broadcasts into the row views)
             dist.all_gather(self.s_blocks, self.s_blocks[r])
         dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
@@ -368,7 +392,8 @@ def measure(args, dev, rank, world, config):
     else:
         N, E, dtype = args.nodes or 10_000_000, args.edges or 50_000_000, torch.float32
     t_setup = time.perf_counter()
-    s = setup(dev, N, E, F, args.gamma, dtype, rank, world, row_align=args.row_align)
+    s = setup(dev, N, E, F, args.gamma, dtype, rank, world, row_align=args.row_align,
+              balance=args.balance)
     layer = Layer(s, dev, world)
     plan = layer.plan
     esz = s["xbuf"].element_size()
@@ -413,7 +438,8 @@ def measure(args, dev, rank, world, config):
                 "glorot weights seed 0)",
         "config": {"workload": workload, "nodes": N, "input_edges": E, "messages": M,
                    "features": F, "heads": H, "channels": C, "row_pitch": s["ldx"],
-                   "parallelism": f"dst-shard x{world}" if world > 1 else "single GPU",
+                   "parallelism": (f"dst-shard x{world} ({args.balance}-balanced)" if world > 1
+                                   else "single GPU"),
                    "hubs": plan.num_hubs, "hub_chunks": plan.num_chunks, **counts},
         "roofline": {"bound": "hbm", "achieved": kernels[dom]["gbps"], "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": kernels[dom]["frac"],
@@ -469,7 +495,7 @@ def launch_ranks(args, argv, device_count=None, run=None) -> int:
     import subprocess
     n = args.gpus
     have = torch.cuda.device_count() if device_count is None else device_count
-    if have < n:
+    if have < n and not args.rehearse:
         log(f"[bench] --gpus {n}: only {have} device(s) visible; refusing to time fewer ranks")
         return 2
     env = dict(os.environ)
@@ -491,13 +517,20 @@ def main():
     if world != args.gpus:
         log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing a mismatched run")
         sys.exit(2)
+    gpu = local % max(torch.cuda.device_count(), 1) if args.rehearse else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(gpu)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    dev = torch.device("cuda", gpu if world > 1 else 0)
     torch.cuda.set_device(dev)
     res, s, layer = measure(args, dev, rank, world, args.config)
+    if args.rehearse:
+        res["rehearsal"] = ("ranks share the visible GPU(s) with a gloo host-staged exchange: "
+                            "a functional run of the N-rank path, not a scaling measurement")
     if world == 1 and rank == 0 and args.config == "c4":
         import bench_legs
         want = [w for w in args.legs.split(",") if w] if not args.no_legs else []

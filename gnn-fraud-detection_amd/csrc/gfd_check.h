@@ -5,10 +5,12 @@
 // entry point then first validates, on the device, every index array its
 // kernels gather through -- rowptr monotone with rowptr[0] = 0 and
 // rowptr[n] = E', col in [0, N), slot descriptors inside their rows, hub
-// chunks inside their hubs, CSC arrays inside [0, N) / [0, E') -- and a
-// violation prints the array, position and value and traps (the launch fails
-// with a HIP error at the next synchronisation), instead of a kernel faulting
-// somewhere inside a gather.  The product library contains none of this.
+// chunks inside their hubs, CSC arrays inside [0, N) / [0, E') -- and the
+// first violation is recorded (array, position, value, printed once) and the
+// entry point returns GFD_ERR_INDEX before any gather kernel is launched,
+// instead of a kernel faulting somewhere inside a gather.  This build
+// synchronises the stream once per call to read the record (the product
+// library never does).  The product library contains none of this.
 #pragma once
 
 #include "gfd_common.h"
@@ -16,16 +18,30 @@
 namespace gfd {
 
 #ifdef GFD_CHECKED
+// first violation of the current check_graph call: {flag, pos, value}
+struct CheckRecord {
+  int flag;
+  int pad;
+  long long pos, val;
+};
+extern __device__ CheckRecord g_check;
 __device__ __forceinline__ void check_fail(const char* what, long long pos, long long val,
                                            long long lo, long long hi) {
-  printf("gfd checked build: %s[%lld] = %lld outside [%lld, %lld)\n", what, pos, val, lo, hi);
-  __builtin_trap();
+  if (atomicCAS(&g_check.flag, 0, 1) == 0) {  // one report per call
+    g_check.pos = pos;
+    g_check.val = val;
+    printf("gfd checked build: %s[%lld] = %lld outside [%lld, %lld)\n", what, pos, val, lo, hi);
+  }
 }
+// in a check kernel's body: record and leave the thread (nothing after a bad
+// index reads through it)
 #define GFD_DCHECK(what, pos, val, lo, hi)                                               \
   do {                                                                                   \
     const long long _v = (long long)(val);                                               \
-    if (_v < (long long)(lo) || _v >= (long long)(hi))                                   \
+    if (_v < (long long)(lo) || _v >= (long long)(hi)) {                                 \
       ::gfd::check_fail(what, (long long)(pos), _v, (long long)(lo), (long long)(hi));   \
+      return;                                                                            \
+    }                                                                                    \
   } while (0)
 #endif
 

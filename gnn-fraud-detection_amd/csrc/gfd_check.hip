@@ -5,6 +5,8 @@
 namespace gfd {
 
 #ifdef GFD_CHECKED
+__device__ CheckRecord g_check;
+
 namespace {
 
 constexpr int kCB = 256;
@@ -13,9 +15,10 @@ __global__ void k_check_rows(const int32_t* __restrict__ rowptr, const int32_t* 
                              int64_t n, int64_t N) {
   const int64_t i = blockIdx.x * int64_t(kCB) + threadIdx.x;
   if (i > n) return;
+  if (i == 0) GFD_DCHECK("rowptr[0] (range start)", 0, rowptr[0], 0, rowptr[n] + 1);
   if (i < n) {
     const int64_t e0 = rowptr[i], e1 = rowptr[i + 1];
-    GFD_DCHECK("rowptr (monotone)", i + 1, e1, e0, 0x7fffffffLL + 1);
+    GFD_DCHECK("rowptr (monotone, <= rowptr[n])", i + 1, e1, e0, int64_t(rowptr[n]) + 1);
     for (int64_t e = e0; e < e1; ++e) GFD_DCHECK("col", e, col[e], 0, N);
   }
 }
@@ -68,6 +71,9 @@ gfd_status check_graph(const int32_t* rowptr, const int32_t* col, int64_t num_ds
                        const gfd_plan* plan, const int32_t* colptr, const int32_t* csc_dst,
                        const int32_t* csc_eid, int64_t num_messages, hipStream_t stream) {
 #ifdef GFD_CHECKED
+  void* rec = nullptr;
+  if (hipGetSymbolAddress(&rec, HIP_SYMBOL(g_check)) != hipSuccess) return GFD_ERR_HIP;
+  if (hipMemsetAsync(rec, 0, sizeof(CheckRecord), stream) != hipSuccess) return GFD_ERR_HIP;
   if (num_dst > 0) {
     k_check_rows<<<blocks(num_dst + 1), kCB, 0, stream>>>(rowptr, col, num_dst, N);
     GFD_LAUNCH_CHECK();
@@ -88,6 +94,11 @@ gfd_status check_graph(const int32_t* rowptr, const int32_t* col, int64_t num_ds
     k_check_csc<<<blocks(N), kCB, 0, stream>>>(colptr, csc_dst, csc_eid, N, num_messages);
     GFD_LAUNCH_CHECK();
   }
+  CheckRecord host{};
+  if (hipMemcpyAsync(&host, rec, sizeof(host), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return GFD_ERR_HIP;
+  if (host.flag) return GFD_ERR_INDEX;
 #else
   (void)rowptr; (void)col; (void)num_dst; (void)N; (void)plan; (void)colptr; (void)csc_dst;
   (void)csc_eid; (void)num_messages; (void)stream;

@@ -4,8 +4,9 @@
 
 Each ``csrc/*.hip`` is compiled to an object in parallel, then linked into
 ``gfd/libgfd.so`` next to this file (git-ignored, shipped to the GPU box by the
-gpurun snapshot).  Rebuilds only when a source or header is newer than the
-library.  No torch involvement: the library is plain HIP + rocPRIM headers.
+gpurun snapshot).  ``--all`` (the driver's ``build()``) also builds the shipped
+variants: ``libgfd_checked.so``, the bounds-checked diagnostic build.  Rebuilds
+only when a source or header is newer than the library.  No torch involvement: the library is plain HIP + rocPRIM headers.
 """
 from __future__ import annotations
 
@@ -25,19 +26,32 @@ INCLUDE = os.path.join(REPO, "include")
 VARIANT = os.environ.get("GFD_BUILD_VARIANT", "")
 if os.environ.get("GFD_EXTRA_FLAGS") and not VARIANT:
     raise RuntimeError("GFD_EXTRA_FLAGS needs GFD_BUILD_VARIANT (never rebuild libgfd.so with A/B flags)")
-LIB = os.path.join(PKG, f"libgfd_{VARIANT}.so" if VARIANT else "libgfd.so")
-OBJDIR = os.path.join(ROOT, "build", f"obj_{VARIANT}" if VARIANT else "obj")
 ARCH = os.environ.get("GFD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 # -fno-honor-nans: fmaxf without operand canonicalisation, so the DPP row
 # rotations fold into v_max_f32_dpp (no kernel relies on NaN semantics)
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-         "-fno-honor-nans",
-         f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
-# GFD_EXTRA_FLAGS: A/B builds into their own library (with GFD_BUILD_VARIANT)
-FLAGS += os.environ.get("GFD_EXTRA_FLAGS", "").split()
+BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+              "-fno-honor-nans",
+              f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
+# the variants build() always produces next to the product library:
+#   checked -- the bounds-checked diagnostic build (gfd_check.h)
+SHIPPED_VARIANTS = {"checked": ["-DGFD_CHECKED"]}
 # Per-source flags (none at present): {"file.hip": [flags]}
 SOURCE_FLAGS = {}
+
+
+def lib_path(variant: str = "") -> str:
+    return os.path.join(PKG, f"libgfd_{variant}.so" if variant else "libgfd.so")
+
+
+def obj_dir(variant: str = "") -> str:
+    return os.path.join(ROOT, "build", f"obj_{variant}" if variant else "obj")
+
+
+# the library this process builds by default (env-selected A/B variant or the product)
+LIB = lib_path(VARIANT)
+OBJDIR = obj_dir(VARIANT)
+FLAGS = BASE_FLAGS + os.environ.get("GFD_EXTRA_FLAGS", "").split()
 
 
 def sources():
@@ -50,43 +64,60 @@ def _deps():
     return hdrs
 
 
-def _compile(src: str) -> str:
-    obj = os.path.join(OBJDIR, os.path.basename(src)[:-4] + ".o")
+def _compile(src: str, objdir: str, flags) -> str:
+    obj = os.path.join(objdir, os.path.basename(src)[:-4] + ".o")
     newest = max(os.path.getmtime(p) for p in [src] + _deps())
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest:
         return obj
-    cmd = [HIPCC, *FLAGS, *SOURCE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+    cmd = [HIPCC, *flags, *SOURCE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
     return obj
 
 
-def needs_build() -> bool:
-    if not os.path.exists(LIB):
+def needs_build(lib: str = None) -> bool:
+    lib = lib or LIB
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     return any(os.path.getmtime(p) > t for p in sources() + _deps())
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
-        return LIB
-    os.makedirs(OBJDIR, exist_ok=True)
+def _build_one(lib: str, objdir: str, flags, force: bool, verbose: bool) -> str:
+    if not force and not needs_build(lib):
+        return lib
+    os.makedirs(objdir, exist_ok=True)
     srcs = sources()
     workers = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(workers) as ex:
-        objs = list(ex.map(_compile, srcs))
-    tmp = LIB + ".tmp"
+        objs = list(ex.map(lambda s: _compile(s, objdir, flags), srcs))
+    tmp = lib + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     if verbose:
-        print(f"[gfd.build] built {LIB} from {len(srcs)} sources for {ARCH}", file=sys.stderr)
-    return LIB
+        print(f"[gfd.build] built {lib} from {len(srcs)} sources for {ARCH}", file=sys.stderr)
+    return lib
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    """The library this process selects (the product, or GFD_BUILD_VARIANT)."""
+    return _build_one(LIB, OBJDIR, FLAGS, force, verbose)
+
+
+def build_all(force: bool = False, verbose: bool = True) -> list:
+    """The product library and every shipped variant (the driver's build())."""
+    out = [_build_one(lib_path(), obj_dir(), BASE_FLAGS, force, verbose)]
+    for name, extra in SHIPPED_VARIANTS.items():
+        out.append(_build_one(lib_path(name), obj_dir(name), BASE_FLAGS + extra, force, verbose))
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--all" in sys.argv:
+        build_all(force="--force" in sys.argv)
+    else:
+        build(force="--force" in sys.argv)

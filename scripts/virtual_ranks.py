@@ -1,0 +1,99 @@
+"""Per-rank compute of bench.py's N-rank path, measured one rank at a time on
+ONE GPU (the driver's 8-GPU scaling run is the real measurement; this is the
+single-GPU estimate of its compute part).
+
+For each rank r of a world of N: bench.setup with the rank's destination
+shard, bench.Layer(world = N) stepped with the two collectives emulated from
+the whole-graph run (the all-gathered s table and max |x| are copied in), and
+the stage times from HIP events, median over --steps.  Prints one JSON line:
+per-rank stage ms, max over ranks of the compute stages, and the whole-graph
+single-GPU step for the ratio.
+
+    python scripts/virtual_ranks.py --world 8 [--balance nodes|messages]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "gnn-fraud-detection_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as tdist  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--world", type=int, default=8)
+    p.add_argument("--balance", choices=["nodes", "messages"], default="nodes")
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--nodes", type=int, default=10_000_000)
+    p.add_argument("--edges", type=int, default=50_000_000)
+    a = p.parse_args()
+    from gfd import dist as gdist
+    dev = torch.device("cuda", 0)
+    s = bench.setup(dev, a.nodes, a.edges, 166)
+    whole = bench.Layer(s, dev, 1)
+    el, whole_ms, _ = bench.time_layer(whole, a.steps, a.warmup, 1)
+    st_full, xmax = whole.st.clone(), whole.xmax.clone()
+    g = s["graph"]
+
+    def all_gather_into_tensor(out, inp, group=None):
+        n = min(out.shape[0], st_full.shape[0])
+        out[:n] = st_full[:n, :8]
+
+    def all_gather(outs, inp, group=None):
+        lo = 0
+        for o in outs:  # uneven views in node order
+            o.copy_(st_full[lo:lo + o.shape[0], :8])
+            lo += o.shape[0]
+
+    def all_reduce(t, op=None, group=None):
+        t.copy_(torch.maximum(t, xmax))
+
+    tdist.all_gather_into_tensor = all_gather_into_tensor
+    tdist.all_gather = all_gather
+    tdist.all_reduce = all_reduce
+    tdist.get_backend = lambda group=None: "nccl"
+    ranks = []
+    for r in range(a.world):
+        sr = dict(s)
+        sr["spec"] = gdist.ShardSpec(g.rowptr, r, a.world, a.balance)
+        sr["shard"] = g.shard(sr["spec"].dst_lo, sr["spec"].dst_hi)
+        layer = bench.Layer(sr, dev, a.world)
+        for _ in range(a.warmup):
+            layer.step()
+        nst = len(layer.stages)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(nst + 1)]
+               for _ in range(a.steps)]
+        for k in range(a.steps):
+            layer.step(evs[k])
+        torch.cuda.synchronize()
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        stage = {name: med([e[k].elapsed_time(e[k + 1]) for e in evs])
+                 for k, (name, _) in enumerate(layer.stages)}
+        compute = sum(v for k, v in stage.items() if k != "exchange")
+        sh = sr["shard"]
+        ranks.append({"rank": r, "dst": [sr["spec"].dst_lo, sr["spec"].dst_hi],
+                      "messages": int(sh.rowptr[-1].item() - sh.rowptr[0].item()),
+                      "stage_ms": stage, "compute_ms": compute})
+        del layer
+        for k in [k for k in g._shards if k != (0, g.num_nodes)]:
+            del g._shards[k]
+        torch.cuda.empty_cache()
+    worst = max(x["compute_ms"] for x in ranks)
+    whole_step = el * 1e3 / a.steps
+    print(json.dumps({"world": a.world, "balance": a.balance, "whole_graph_ms": whole_step,
+                      "whole_stage_ms": whole_ms, "max_rank_compute_ms": worst,
+                      "compute_speedup_bound": whole_step / worst,
+                      "note": "exchange (RCCL all-gather of N x 32 B + max all-reduce) not "
+                              "included: it needs the 8-GPU node", "ranks": ranks}))
+
+
+if __name__ == "__main__":
+    main()

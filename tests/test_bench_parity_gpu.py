@@ -107,13 +107,14 @@ def test_c4_dst_shards(c4, world):
         del g._shards[k]
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_bench_multi_rank_path(world, monkeypatch):
+@pytest.mark.parametrize("world,balance", [(2, "nodes"), (8, "nodes"), (8, "messages")])
+def test_bench_multi_rank_path(world, balance, monkeypatch):
     """bench.Layer's N > 1 path (the one the driver's scaling run times), rank by
     rank on this GPU with the two collectives emulated from the whole-graph
     run: the fused logits + lone pass over the rank's destinations, the
-    all-gather-v of the source logits, the shard's tile stage.  Every rank's
-    rows equal the single-GPU layer's."""
+    all-gather of the source logits (node balance: equal blocks, in place into
+    the padded table; message balance: uneven row views), the shard's tile
+    stage.  Every rank's rows equal the single-GPU layer's."""
     import bench
     import torch.distributed as tdist
     from gfd import dist as gdist
@@ -123,10 +124,12 @@ def test_bench_multi_rank_path(world, monkeypatch):
     whole.step()
     torch.cuda.synchronize()
     ref, st_full, xmax = whole.out.clone(), whole.st.clone(), whole.xmax.clone()
-    bounds = gdist.edge_balanced_bounds(g.rowptr, world)
+    spec0 = gdist.ShardSpec(g.rowptr, 0, world, balance)
+    bounds, per = spec0.dst_bounds, spec0.per
     sent = []
 
     def all_gather(outs, inp, group=None):
+        assert balance == "messages"
         # the rank's own block is the input (in place): its rows must already
         # hold the fused logits pass's s, the other blocks land at their rows
         assert len(outs) == world
@@ -138,7 +141,14 @@ def test_bench_multi_rank_path(world, monkeypatch):
         sent.append(me)
 
     def all_gather_into_tensor(out, inp, group=None):
-        raise AssertionError("edge-balanced blocks are uneven: the list form is expected")
+        assert balance == "nodes", "message-balanced blocks are uneven: the list form is expected"
+        assert out.shape == (world * per, H) and inp.shape == (per, H)
+        me = (inp.data_ptr() - out.data_ptr()) // (4 * H * per)   # in place: the rank's slot
+        assert inp.data_ptr() == out[me * per:].data_ptr()
+        lo, hi = bounds[me], bounds[me + 1]
+        assert torch.equal(inp[:hi - lo], st_full[lo:hi, :H])
+        out[:g.num_nodes] = st_full[:, :H]
+        sent.append(int(me))
 
     def all_reduce(t, op=None, group=None):
         t.copy_(torch.maximum(t, xmax))
@@ -146,16 +156,17 @@ def test_bench_multi_rank_path(world, monkeypatch):
     monkeypatch.setattr(tdist, "all_gather", all_gather)
     monkeypatch.setattr(tdist, "all_gather_into_tensor", all_gather_into_tensor)
     monkeypatch.setattr(tdist, "all_reduce", all_reduce)
+    monkeypatch.setattr(tdist, "get_backend", lambda group=None: "nccl")
     for r in range(world):
         sr = dict(s)
-        sr["spec"] = gdist.ShardSpec(g.rowptr, r, world)
+        sr["spec"] = gdist.ShardSpec(g.rowptr, r, world, balance)
         sr["shard"] = g.shard(sr["spec"].dst_lo, sr["spec"].dst_hi)
         layer = bench.Layer(sr, DEV, world)
         layer.step()
         torch.cuda.synchronize()
         lo, hi = sr["spec"].dst_lo, sr["spec"].dst_hi
         # s | t of the own rows from the fused pass: bit-identical per-row arithmetic
-        assert torch.equal(layer.s_all, st_full[:, :H]), f"rank {r}: gathered s table"
+        assert torch.equal(layer.s_all[:g.num_nodes], st_full[:, :H]), f"rank {r}: s table"
         assert torch.equal(layer.t_loc[:hi - lo], st_full[lo:hi, H:]), f"rank {r}: own t"
         assert sent[-1] == r
         assert_close(layer.out[:hi - lo], ref[lo:hi], atol=1e-5, rtol=1e-5,

@@ -418,17 +418,94 @@ def test_full_size_sampled_parity_and_invariants():
     assert_close(out[lone.to(DEV)], ref_lone.detach(), what="self-loop-only rows")
 
 
+def _checked_lib():
+    import os
+    from gfd import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libgfd_checked.so")
+    assert os.path.exists(path), "libgfd_checked.so missing: __graft_entry__.build() ships it"
+    return _lib.open_variant(path)
+
+
+@pytest.mark.parametrize("corrupt", ["col", "rowptr", "slot_desc", "csc_dst"])
+def test_checked_build_rejects_bad_indices(corrupt):
+    """The checked build validates every index array before any gather kernel
+    runs: one corrupted entry (a source >= N, a rowptr past the end, a slot
+    descriptor of another row, a CSC destination >= N) makes the forward /
+    backward return GFD_ERR_INDEX instead of faulting inside a gather, and the
+    output buffer is not touched."""
+    from gfd import _lib
+    chk = _checked_lib()
+    _, graph = _gfd()
+    N, F = 3000, 64
+    x, ei, conv = _random_case(N, 20000, F, seed=32)
+    g = graph.get_graph(ei.to(DEV), N)
+    plan, csc = g.plan(), g.csc()
+    rowptr, col = g.rowptr.clone(), g.col.clone()
+    desc = plan.slot_desc.clone() if plan.slot_desc is not None else None
+    cdst = csc.dst.clone()
+    if corrupt == "col":
+        col[len(col) // 2] = N
+    elif corrupt == "rowptr":
+        rowptr[N // 2] = rowptr[-1] + 7
+    elif corrupt == "slot_desc":
+        desc.view(-1, 4)[N // 3, 1] += 1           # e_begin no longer its row's start
+    else:
+        cdst[5] = N + 3
+    plan.cstruct()
+    pc = _lib.GfdPlan.from_buffer_copy(plan._c)
+    if corrupt == "slot_desc":
+        pc.slot_desc = desc.data_ptr()
+    cp = _lib.ct.byref(pc)
+    xd = x.to(DEV).contiguous()
+    W = conv.lin_src.weight.detach().to(DEV).contiguous()
+    a_s = conv.att_src.detach().to(DEV).reshape(-1).contiguous()
+    a_d = conv.att_dst.detach().to(DEV).reshape(-1).contiguous()
+    b = conv.bias.detach().to(DEV)
+    stream = _lib.stream_handle(DEV)
+    out = torch.full((N, 64), 7.0, device=DEV)
+    st = torch.zeros(N, 16, device=DEV)
+    ws = torch.empty(chk.gfd_gat_fwd_workspace_size(N, N, F, 8, 64, plan.num_hubs, plan.num_chunks),
+                     dtype=torch.uint8, device=DEV)
+    if corrupt != "csc_dst":
+        rc = chk.gfd_gat_fwd(xd.data_ptr(), 0, N, F, F, rowptr.data_ptr(), col.data_ptr(),
+                             W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), b.data_ptr(), 8, 64, 0.2,
+                             0.0, 0, cp, out.data_ptr(), st.data_ptr(), None, ws.data_ptr(),
+                             ws.numel(), stream)
+        torch.cuda.synchronize()
+        assert rc == 2, f"checked forward returned {rc} for a corrupted {corrupt}"
+        assert torch.all(out == 7.0), "no kernel may write the output after a failed check"
+        return
+    # backward over a valid forward, the CSC corrupted
+    stats = torch.empty(N, 16, device=DEV)
+    assert chk.gfd_gat_fwd(xd.data_ptr(), 0, N, F, F, rowptr.data_ptr(), col.data_ptr(),
+                           W.data_ptr(), a_s.data_ptr(), a_d.data_ptr(), b.data_ptr(), 8, 64, 0.2,
+                           0.0, 0, cp, out.data_ptr(), st.data_ptr(), stats.data_ptr(),
+                           ws.data_ptr(), ws.numel(), stream) == 0
+    go = torch.randn(N, 64, device=DEV)
+    gw = torch.full_like(W, 7.0)
+    ga, gd = torch.empty_like(a_s), torch.empty_like(a_d)
+    gb = torch.empty(64, device=DEV)
+    bws = torch.empty(chk.gfd_gat_bwd_workspace_size(N, g.num_messages, F, 8, 64, plan.num_hubs,
+                                                     plan.num_chunks, csc.plan.num_chunks),
+                      dtype=torch.uint8, device=DEV)
+    rc = chk.gfd_gat_bwd(xd.data_ptr(), 0, N, F, F, rowptr.data_ptr(), col.data_ptr(), cp,
+                         csc.colptr.data_ptr(), cdst.data_ptr(), csc.eid.data_ptr(),
+                         csc.plan.cstruct(), g.num_messages, W.data_ptr(), a_s.data_ptr(),
+                         a_d.data_ptr(), 8, 64, 0.2, 0.0, 0, st.data_ptr(), stats.data_ptr(),
+                         go.data_ptr(), None, gw.data_ptr(), ga.data_ptr(), gd.data_ptr(),
+                         gb.data_ptr(), bws.data_ptr(), bws.numel(), stream)
+    torch.cuda.synchronize()
+    assert rc == 2, f"checked backward returned {rc} for a corrupted csc_dst"
+    assert torch.all(gw == 7.0)
+
+
 def test_checked_build_accepts_valid_graphs():
     """The bounds-checked diagnostic build (-DGFD_CHECKED, libgfd_checked.so:
     every index array validated on the device before the kernels run) gives
     the product library's forward and backward on a valid graph with hubs and
-    every class (no false positives).  Skipped when the variant was not built."""
-    import os
+    every class (no false positives).  build() ships the variant."""
     from gfd import _lib
-    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libgfd_checked.so")
-    if not os.path.exists(path):
-        pytest.skip("libgfd_checked.so not built (GFD_BUILD_VARIANT=checked GFD_EXTRA_FLAGS=-DGFD_CHECKED)")
-    chk = _lib.open_variant(path)
+    chk = _checked_lib()
     prod = _lib.load()
     _, graph = _gfd()
     N, F = 6000, 166
