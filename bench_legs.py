@@ -134,6 +134,7 @@ def c2_gat3_train_step(dev, steps=20, warmup=3, cpu_runs=3):
         ropt.step()
         times.append(time.perf_counter() - t0)
     tt = sorted(times[1:])
+    err = _c2_parity(m, d, mask, yl, dev)
     return {"workload": f"GAT 3 layers train step (fwd + BCE(pos_weight 50) + bwd + Adam), "
                         f"Elliptic-shaped N={d['N']} E={d['E']} F=165, dropout 0.2",
             "unit": "edges/s", "value": d["E"] / (med * 1e-3), "ms_per_step": med,
@@ -142,7 +143,54 @@ def c2_gat3_train_step(dev, steps=20, warmup=3, cpu_runs=3):
                              "median_s": tt[len(tt) // 2], "min_s": tt[0], "runs": cpu_runs,
                              "cores": torch.get_num_threads(), "kind": "port",
                              "sample": "the whole C2 graph: oracle GATRef train step (PyG CPU "
-                                       "dataflow + torch autograd + Adam), same weights"}}
+                                       "dataflow + torch autograd + Adam), same weights"},
+            **err}
+
+
+def _c2_parity(m, d, mask, yl, dev):
+    """One fwd + BCE + bwd step of the leg's weights with dropout 0 (the
+    counter-based masks are not torch's RNG stream) on the device and in the
+    oracle: max |logits error| and the largest gradient error relative to its
+    tensor's max (tests/test_fullsize_models_gpu.py asserts the same bounds)."""
+    from gfd.models import GAT
+    from oracle import GATRef
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    g = GAT(165, 64, 1, num_layers=3, dropout=0.0)
+    g.load_state_dict(sd, strict=True)
+    g = g.to(dev).train()
+    r = GATRef(165, 64, 1, num_layers=3, dropout=0.0).train()
+    r.load_state_dict(sd, strict=True)
+    x = d["x"].clone().requires_grad_(True)
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0], device=dev))
+    lg = g(x, d["edge_index"])
+    crit(lg[mask].squeeze(1), yl).backward()
+    xr = d["x"].cpu().requires_grad_(True)
+    lr = r(xr, d["edge_index"].cpu())
+    torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0]))(
+        lr[mask.cpu()].squeeze(1), yl.cpu()).backward()
+    rp = dict(r.named_parameters())
+    rel = [(x.grad.cpu() - xr.grad).abs().max().item() / xr.grad.abs().max().item()]
+    zero, tol = [], [0.0]
+    for name, p in g.named_parameters():
+        if p.grad is None or name.endswith("lin_dst.weight"):
+            continue
+        err = (p.grad.cpu() - rp[name].grad).abs().max().item()
+        den = rp[name].grad.abs().max().item()
+        tol.append(err / (2e-4 * den + 1e-5))   # the test's bound (tests/_util.py)
+        if den < 1e-6:   # analytically zero: a GATConv bias under train-mode BatchNorm
+            zero.append(name)
+        else:
+            rel.append(err / den)
+    return {"max_abs_err_vs_oracle": (lg.detach().cpu() - lr.detach()).abs().max().item(),
+            "max_grad_rel_err_vs_oracle": max(rel),
+            "max_grad_err_over_tolerance": max(tol),
+            "zero_grad_params": zero,
+            "parity_note": "dropout 0 step, same weights: logits max abs error; gradients: max "
+                           "|error| / max |oracle grad| over x and every parameter whose "
+                           "gradient is not analytically zero (zero_grad_params: biases "
+                           "feeding train-mode BatchNorm, where both sides are rounding "
+                           "noise); max_grad_err_over_tolerance <= 1: every gradient within "
+                           "2e-4 max|ref| + 1e-5"}
 
 
 def c3_tgn_49_steps(dev, steps=20, warmup=3, cpu_runs=3):
@@ -162,13 +210,18 @@ def c3_tgn_49_steps(dev, steps=20, warmup=3, cpu_runs=3):
     ts, ei = d["time_step"].cpu().numpy(), d["edge_index"].cpu().numpy()
     t0s, t1s = int(ts.min()), int(ts.max())
     times = []
+    err = 0.0
     with torch.no_grad():
-        for _ in range(1 + cpu_runs):
+        got = m.forward_snapshots(d["x"], d["edge_index"], d["time_step"])[0].cpu()
+        for it in range(1 + cpu_runs):
             c0 = time.perf_counter()
+            outs = []
             for t in range(t0s, t1s + 1):
                 nodes, loc, _ = temporal_subgraph_ref(ts, ei, t)
-                ref(xc[torch.from_numpy(nodes)], torch.from_numpy(loc))
+                outs.append((nodes, ref(xc[torch.from_numpy(nodes)], torch.from_numpy(loc))[0]))
             times.append(time.perf_counter() - c0)
+        for nodes, ro in outs:   # the last run's per-step outputs against the device's
+            err = max(err, (got[torch.from_numpy(nodes)] - ro).abs().max().item())
     tt = sorted(times[1:])
     return {"workload": f"TemporalGNN 3 layers, forward over the 49 time-step snapshots "
                         f"(h0 = 0 per step), N={d['N']} E={d['E']} F=165, eval",
@@ -178,7 +231,8 @@ def c3_tgn_49_steps(dev, steps=20, warmup=3, cpu_runs=3):
                              "median_s": tt[len(tt) // 2], "min_s": tt[0], "runs": cpu_runs,
                              "cores": torch.get_num_threads(), "kind": "port",
                              "sample": "the whole C3 workload: per step snapshot extraction "
-                                       "(numpy) + oracle TemporalGNNRef (PyG CPU dataflow)"}}
+                                       "(numpy) + oracle TemporalGNNRef (PyG CPU dataflow)"},
+            "max_abs_err_vs_oracle": err}
 
 
 def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2, dropout=0.0):

@@ -1,0 +1,116 @@
+"""Full-size parity of configs C2 and C3 (BASELINE.json configs[1], [2]) on the
+whole Elliptic-shaped graph the reference trains and evaluates on (203,769
+nodes / 234,355 edges / 165 features, 49 time steps; gfd.synth.elliptic_like,
+the shape of train.py:95-143 and tgn.py:67-113), with the reference's shipped
+checkpoint weights (tests/golden/elliptic_small.npz, written by
+make_golden.py from results/{gat,tgn}_model.pt).
+
+* C2: one training step of train.py:115-142 -- 3-layer GAT in train mode
+  (BatchNorm batch statistics over all 203,769 rows), dropout 0 for parity,
+  BCEWithLogits(pos_weight = 50) over the labelled nodes, backward -- on the
+  device (libgfd.so) against oracle.GATRef + torch autograd on the CPU: logits,
+  loss, grad_x, every parameter gradient, and the BatchNorm running statistics
+  the step updates.  (Adam itself is torch.optim on both sides, consuming these
+  gradients.)
+* C3: TemporalGNN (3 layers + GRUCell(h, 0) + Linear) over the 49 time-step
+  snapshots, eval mode: gfd's one-pass forward_snapshots against
+  oracle.TemporalGNNRef run step by step on each snapshot the reference's
+  create_temporal_subgraph (dataset.py:198-240, oracle.temporal_ref) extracts;
+  plus the whole-graph forward.
+Tolerances as tests/_util.py: forward 1e-4 (+1e-4 relative), gradients 2e-4 of
+each tensor's max (three train-mode BatchNorms), as the fixture-size tests."""
+import numpy as np
+import pytest
+import torch
+
+from _util import assert_close, assert_close_scaled, state_dict_from
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def elliptic():
+    from gfd import synth
+    d = synth.elliptic_like(num_features=165, seed=0)
+    assert d["x"].shape == (203_769, 165) and d["edge_index"].shape == (2, 234_355)
+    return d
+
+
+def _pair(kind, golden, prefix, train):
+    from gfd.models import GAT, TemporalGNN
+    from oracle import GATRef, TemporalGNNRef
+    arr = golden("elliptic_small.npz")
+    sd = state_dict_from(arr, prefix)
+    cls, rcls = (GAT, GATRef) if kind == "gat" else (TemporalGNN, TemporalGNNRef)
+    m = cls(in_channels=165, hidden_channels=64, out_channels=1, num_layers=3, dropout=0.0)
+    m.load_state_dict(sd, strict=True)
+    ref = rcls(165, 64, 1, num_layers=3, dropout=0.0)
+    ref.load_state_dict({k: v.clone() for k, v in sd.items()}, strict=True)
+    m = m.to(DEV)
+    return (m.train(), ref.train()) if train else (m.eval(), ref.eval())
+
+
+def test_c2_full_size_train_step_matches_oracle(elliptic, golden):
+    m, ref = _pair("gat", golden, "gat.", train=True)
+    y = torch.from_numpy(elliptic["y"])
+    mask = y != -1
+    yl = y[mask].float()
+    ei = torch.from_numpy(elliptic["edge_index"])
+    # device step
+    x = torch.from_numpy(elliptic["x"]).to(DEV).requires_grad_(True)
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0], device=DEV))
+    logits = m(x, ei.to(DEV))
+    loss = crit(logits[mask.to(DEV)].squeeze(1), yl.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    # oracle step (PyG CPU dataflow + autograd), same weights and inputs
+    xr = torch.from_numpy(elliptic["x"]).requires_grad_(True)
+    rcrit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0]))
+    rlogits = ref(xr, ei)
+    rloss = rcrit(rlogits[mask].squeeze(1), yl)
+    rloss.backward()
+    assert_close(logits.detach(), rlogits.detach(), what="C2 full-size train logits")
+    assert abs(loss.item() - rloss.item()) <= 1e-4 * max(1.0, abs(rloss.item())), \
+        (loss.item(), rloss.item())
+    assert_close_scaled(x.grad, xr.grad, rtol=2e-4, what="C2 grad_x")
+    rparams = dict(ref.named_parameters())
+    checked = 0
+    for name, p in m.named_parameters():
+        if name.endswith("lin_dst.weight"):
+            continue
+        assert_close_scaled(p.grad, rparams[name].grad, rtol=2e-4, atol=1e-5, what=f"C2 grad {name}")
+        checked += 1
+    assert checked >= 15
+    rbufs = dict(ref.named_buffers())
+    for name, b in m.named_buffers():
+        if b.dtype.is_floating_point:
+            assert_close(b, rbufs[name], what=f"C2 BatchNorm buffer {name} after the step")
+
+
+def test_c3_full_size_49_snapshots_match_oracle(elliptic, golden):
+    from oracle.temporal_ref import temporal_subgraph_ref
+    m, ref = _pair("tgn", golden, "tgn.", train=False)
+    x = torch.from_numpy(elliptic["x"])
+    ei = torch.from_numpy(elliptic["edge_index"])
+    ts = torch.from_numpy(elliptic["time_step"])
+    with torch.no_grad():
+        out, hid = m.forward_snapshots(x.to(DEV), ei.to(DEV), ts.to(DEV))
+        out, hid = out.cpu(), hid.cpu()
+        tsn, ein = ts.numpy(), ei.numpy()
+        steps = range(int(tsn.min()), int(tsn.max()) + 1)
+        assert len(steps) == 49
+        worst = 0.0
+        for t in steps:   # the reference's per-step loop: snapshot + forward with h0 = 0
+            nodes, loc, _ = temporal_subgraph_ref(tsn, ein, t)
+            nodes = torch.from_numpy(nodes)
+            ro, rh = ref(x[nodes], torch.from_numpy(loc))
+            assert_close(out[nodes], ro, what=f"C3 step {t} out ({nodes.numel()} nodes)")
+            assert_close(hid[nodes], rh, what=f"C3 step {t} hidden")
+            worst = max(worst, (out[nodes] - ro).abs().max().item())
+        # the whole-graph forward (edges never cross steps: the same outputs)
+        gout, ghid = m(x.to(DEV), ei.to(DEV))
+        rout, rhid = ref(x, ei)
+    assert_close(gout.cpu(), rout, what="C3 whole-graph out")
+    assert_close(ghid.cpu(), rhid, what="C3 whole-graph hidden")
+    assert worst < 1e-4
