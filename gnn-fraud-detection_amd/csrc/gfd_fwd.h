@@ -114,6 +114,9 @@ __device__ __forceinline__ f32x4 load4(const typename XT::T* p) {
 // in bytes < 2^32 (checked on the host)
 template <typename XT>
 __device__ __forceinline__ const char* xrow(const void* x, int j, int64_t ldx) {
+#ifdef GFD_AB_NOGATHER
+  j &= 1023;  // ablation build only: every gathered row from a 1,024-row (L2) window
+#endif
   return reinterpret_cast<const char*>(x) +
          uint64_t(uint32_t(j)) * uint64_t(uint32_t(ldx) * uint32_t(XT::kBytes));
 }
