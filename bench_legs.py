@@ -261,23 +261,40 @@ def c4_layer_fwd_bwd(s, dev, steps=5, warmup=2, dropout=0.0):
     bwd_ms = med - fwd_med
     nbytes = bwd_algorithmic_bytes(g.num_nodes, g.num_messages, s["x"].shape[1],
                                    s["x"].element_size())
+    dbytes = bwd_design_bytes(g.num_nodes, g.num_messages, s["x"].shape[1],
+                              s["x"].element_size())
     return {"workload": f"C4 GATConv layer 0 forward (training stats) + backward (grad W, att, "
                         f"bias; no grad_x), N={g.num_nodes} E={E}, attention dropout {dropout}",
             "unit": "edges/s",
             "value": E / (med * 1e-3), "ms_per_step": med, "ms_mean": mean,
             "forward_ms": fwd_med, "backward_ms": bwd_ms,
-            # the whole backward pass against HBM: its algorithmic bytes (DESIGN.md
-            # §5, bwd_algorithmic_bytes) over backward_ms (one C-ABI call; its
-            # kernels' split is in profiles/r3c_bwd_kernel_top25.txt)
+            # the whole backward pass against HBM: the MINIMAL x-space bytes
+            # (bwd_algorithmic_bytes) over backward_ms (one C-ABI call; its
+            # kernels' split in profiles/); this design's own bytes (its 64-B
+            # message records and dh' rows written and re-read) as design_bytes,
+            # the PMC counter bytes as traffic
             "roofline": {"bound": "hbm", "scope": "backward pass", "achieved":
                          nbytes / (bwd_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": nbytes / (bwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                         "algorithmic_bytes": nbytes, "traffic": None}}
+                         "algorithmic_bytes": nbytes, "design_bytes": dbytes,
+                         "design_gbps": dbytes / (bwd_ms * 1e-3) / 1e9, "traffic": None}}
 
 
-def bwd_algorithmic_bytes(N, M, F, es, C=64, kdh=528):
-    """Minimum HBM bytes of one GATConv backward (grad W, att, bias) in this
-    formulation: per message (M, self loops included) the x_j row, its index
+def bwd_algorithmic_bytes(N, M, F, es, C=64, H=8):
+    """Minimal HBM bytes of one GATConv backward (grad W, att, bias), in x
+    space and independent of this implementation's intermediates: per message
+    (M, self loops included) one x_j row and its CSR index (the attention
+    gradient dA_ijh = <W_h^T g_i, x_j>) and one g_i row and its CSC index (the
+    source-side y_j = sum alpha g_i); per node its x row, g row, logits (s | t)
+    and softmax statistics (max | sum) once, rowptr and colptr.  (At C4: 66 GB.)"""
+    per_msg = (es * F + 4) + (4 * C + 4)
+    per_node = es * F + 4 * C + 4 * 2 * H + 4 * 2 * H + 4 + 4
+    return float(M) * per_msg + float(N) * per_node
+
+
+def bwd_design_bytes(N, M, F, es, C=64, kdh=528):
+    """HBM bytes of this implementation's backward (its own intermediates
+    included): per message (M, self loops included) the x_j row, its index
     and source logits and the 64-B record written (k_bwd_msg), then the CSC
     entry, the record and the g_i row (k_bwd_src); per node the g row, logits
     and softmax stats, dt (k_bwd_msg), the x row (k_xmax), the dh' row written
