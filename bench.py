@@ -184,8 +184,8 @@ class Layer:
             _lib.call("gfd_gat_logits_lone_split", x[spec.dst_lo:].data_ptr(), self.xdt, n, F,
                       s["ldx"], self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
                       s["bias"].data_ptr(), 0.2, self.s_all[spec.dst_lo:].data_ptr(), H,
-                      self.t_loc.data_ptr(), H, self.xmax.data_ptr(), self.out.data_ptr(), None,
-                      self.stream)
+                      self.t_loc.data_ptr(), H, self.xmax.data_ptr(), self.out.data_ptr(), C,
+                      None, self.stream)
 
     def exchange(self):
         # ONE all-gather-v of the [N, 8] source logits (RCCL; uneven blocks land
@@ -227,7 +227,7 @@ class Layer:
                        self.n_dst, s["spec"].dst_lo, self.s_all.data_ptr(), H,
                        self.t_loc.data_ptr(), H, self.xmax.data_ptr(), self.packed.data_ptr(),
                        s["bias"].data_ptr(), H, C, 0.2, 0.0, 0, self.cplan, stages, None,
-                       self.out.data_ptr(), None, self.ws.data_ptr(), self.ws.numel(),
+                       self.out.data_ptr(), C, None, self.ws.data_ptr(), self.ws.numel(),
                        self.stream)
 
     STAGES_FUSED = (("pack+logits+lone", None), ("hubs", STAGE_HUBS), ("general", STAGE_MID),

@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(1024, OCC) k_fused(
     for (int q = 0; q < 4; ++q) {
       const int r = (lane >> 4) * 4 + q;
       const int ri = rowid[r];
-      if (ri >= 0) out[int64_t(ri) * C + n] = epi_store_value(accv[q] * (rscale[r] * wu), b, n, ri, ep);
+      if (ri >= 0) out[int64_t(ri) * ep.ldo + n] = epi_store_value(accv[q] * (rscale[r] * wu), b, n, ri, ep);
     }
   }
 }

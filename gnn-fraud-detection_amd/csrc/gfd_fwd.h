@@ -465,6 +465,7 @@ struct Epi {
   int relu;
   const float* res;
   int64_t ldr;
+  int64_t ldo = C;  // output row stride (floats): out row i at out + i * ldo
 };
 
 __device__ __forceinline__ float epi_store_value(float v, float bias_n, int n, int64_t row,

@@ -175,8 +175,9 @@ gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t N, int F,
                                    const float* t_log, int64_t t_stride, const float* xmax,
                                    const void* packed, const float* bias, int heads, int channels,
                                    float slope, float dp, uint64_t seed, const gfd_plan* plan,
-                                   int stages, const gfd_epilogue* ep, float* out, float* stats,
-                                   void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+                                   int stages, const gfd_epilogue* ep, float* out,
+                                   int64_t out_stride, float* stats, void* ws, size_t ws_bytes,
+                                   gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   const gfd_plan p = plan_or_empty(plan);
@@ -184,7 +185,8 @@ gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t N, int F,
       check_agg_args(x, x_dtype, N, F, ldx, rowptr, col, num_dst, dst_offset, dp, p, out);
   if (s != GFD_OK) return s;
   if (!s_log || !t_log || !packed || stages < 1 || stages > 31) return GFD_ERR_ARGUMENT;
-  if (s_stride < H || t_stride < H || s_stride > (1 << 20) || t_stride > (1 << 20))
+  if (s_stride < H || t_stride < H || s_stride > (1 << 20) || t_stride > (1 << 20) ||
+      out_stride < channels)
     return GFD_ERR_ARGUMENT;
   Epi e{nullptr, 0, nullptr, 0};
   if (ep) {  // inference epilogue (see gfd_gat_fwd_ep); residual rows indexed like out
@@ -192,6 +194,7 @@ gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t N, int F,
     if (ep->residual && ep->residual_stride < channels) return GFD_ERR_ARGUMENT;
     e = Epi{ep->scale_shift, ep->relu ? 1 : 0, ep->residual, ep->residual_stride};
   }
+  e.ldo = out_stride;
   if (num_dst == 0) return GFD_OK;
   const PackLayout L = pack_layout(F);
   s = check_graph(rowptr, col, num_dst, N, plan, nullptr, nullptr, nullptr, 0, stream);
@@ -217,7 +220,7 @@ gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t N, int F, in
   if (!st || dst_offset < 0) return GFD_ERR_ARGUMENT;
   return gfd_gat_aggregate_split(x, x_dtype, N, F, ldx, rowptr, col, num_dst, dst_offset, st, 16,
                                  st + dst_offset * 16 + H, 16, xmax, packed, bias, heads,
-                                 channels, slope, dp, seed, plan, stages, ep, out, stats, ws,
+                                 channels, slope, dp, seed, plan, stages, ep, out, C, stats, ws,
                                  ws_bytes, stream_);
 }
 

@@ -198,7 +198,7 @@ k_logits_lone(
         const int64_t orow = t * 16 + src;
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
-          out[orow * C + ct * 16 + rl] =
+          out[orow * ep.ldo + ct * 16 + rl] =
               epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl, orow, ep);
         if (__builtin_expect(stats != nullptr, 0) && rl < H) {  // training (no dropout) only
           stats[orow * 16 + rl] = leaky(sv[q] + tq, slope);
@@ -273,19 +273,22 @@ gfd_status gfd_gat_logits_lone_split(const void* x, int x_dtype, int64_t num_nod
                                      int heads, int channels, const int32_t* rowptr,
                                      const float* bias, float negative_slope, float* s,
                                      int64_t s_stride, float* t, int64_t t_stride, float* xmax,
-                                     float* out, float* stats, gfd_stream_t stream_) {
+                                     float* out, int64_t out_stride, float* stats,
+                                     gfd_stream_t stream_) {
   if (heads != H || channels != C || in_features < 1 || in_features > 256)
     return GFD_ERR_UNSUPPORTED;
   if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
   if (num_nodes < 0 || x_stride < in_features) return GFD_ERR_ARGUMENT;
-  if (s_stride < H || t_stride < H || s_stride > (1 << 20) || t_stride > (1 << 20))
+  if (s_stride < H || t_stride < H || s_stride > (1 << 20) || t_stride > (1 << 20) ||
+      out_stride < C)
     return GFD_ERR_ARGUMENT;
   if (num_nodes > 0 && (!x || !packed || !rowptr || !s || !t || !out)) return GFD_ERR_ARGUMENT;
   const PackLayout L = pack_layout(in_features);
   return launch_logits_lone(x, x_dtype, num_nodes, in_features, x_stride, L,
                             static_cast<const char*>(packed), rowptr, bias, negative_slope, s,
                             int(s_stride), t, int(t_stride), xmax, out, stats,
-                            Epi{nullptr, 0, nullptr, 0}, static_cast<hipStream_t>(stream_));
+                            Epi{nullptr, 0, nullptr, 0, out_stride},
+                            static_cast<hipStream_t>(stream_));
 }
 
 gfd_status gfd_gat_logits_lone(const void* x, int x_dtype, int64_t num_nodes, int in_features,
@@ -296,7 +299,7 @@ gfd_status gfd_gat_logits_lone(const void* x, int x_dtype, int64_t num_nodes, in
   if (num_nodes > 0 && !st) return GFD_ERR_ARGUMENT;
   return gfd_gat_logits_lone_split(x, x_dtype, num_nodes, in_features, x_stride, packed, heads,
                                    channels, rowptr, bias, negative_slope, st, 16,
-                                   st ? st + H : nullptr, 16, xmax, out, stats, stream_);
+                                   st ? st + H : nullptr, 16, xmax, out, C, stats, stream_);
 }
 
 }  // extern "C"

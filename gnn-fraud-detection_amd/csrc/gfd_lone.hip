@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(kLWaves * 64) k_lone(
       if (orow >= 0) {
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
-          out[int64_t(orow) * C + ct * 16 + r] =
+          out[int64_t(orow) * ep.ldo + ct * 16 + r] =
               epi_store_value(acc[ct][q] * ou, bc[ct], ct * 16 + r, orow, ep);
       }
     }

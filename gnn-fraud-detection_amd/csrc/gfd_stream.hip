@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     for (int q = 0; q < 4; ++q) {
       const int r = (lane >> 4) * 4 + q;
       const int ri = rid[r];
-      if (ri >= 0) out[int64_t(ri) * C + n] = epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep);
+      if (ri >= 0) out[int64_t(ri) * ep.ldo + n] = epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep);
     }
   };
   f32x4 acc_prev = {0.f, 0.f, 0.f, 0.f};  // kh = 0: tile v - 1, stored during MFMA(v)

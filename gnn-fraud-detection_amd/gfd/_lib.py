@@ -98,9 +98,10 @@ SIGNATURES = {
     "gfd_gat_aggregate_split": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, c_i64, c_i64,
                                         P, c_i64, P, c_i64, P, P, P, ct.c_int, ct.c_int, c_f32,
                                         c_f32, c_u64, PLAN, ct.c_int, ct.POINTER(GfdEpilogue), P,
-                                        P, P, c_sz, P]),
+                                        c_i64, P, P, c_sz, P]),
     "gfd_gat_logits_lone_split": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, ct.c_int,
-                                          ct.c_int, P, P, c_f32, P, c_i64, P, c_i64, P, P, P, P]),
+                                          ct.c_int, P, P, c_f32, P, c_i64, P, c_i64, P, P, c_i64,
+                                          P, P]),
     "gfd_gat_fwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,
                             ct.c_int, c_f32, c_f32, c_u64, PLAN, P, P, P, P, c_sz, P]),
     "gfd_gat_fwd_ep": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,

@@ -11,9 +11,25 @@ reference; for a power-law graph that is nearly all of x).  Only the SOURCE
 logits s_j cross GPUs (``exchange_logits``): each rank computes ``[s | t]`` for
 its own destination block (whose t it is the only reader of) and all-gathers
 the s half (``[N, H]`` fp32: 32 B per node instead of the 664 B feature row --
-the "halo" of the north star).  The fused aggregate-project kernels then run on the local shard
-with no further communication.  Hidden layers all-gather the previous layer's
-``[N, 64]`` output instead.
+the "halo" of the north star).  The fused aggregate-project kernels then run on
+the local shard with no further communication.  Hidden layers all-gather the
+previous layer's ``[N, 64]`` output rows together with the next layer's s.
+
+Layout (the split logits ABI, gfd_gat_aggregate_split): every exchanged table
+is laid out by node row, each rank's block where the all-gather puts it, so
+the collective writes straight into the tensors the kernels read -- no scatter
+or concatenation between a collective and the next kernel:
+  * equal blocks (``balance="nodes"``): a ``[world * per, cols]`` table, rank
+    r's rows at ``r * per``; the collective is one in-place
+    ``all_gather_into_tensor`` (RCCL and gloo alike);
+  * message-balanced (uneven) blocks: a ``[N, cols]`` table with rank r's rows
+    at its destination range; RCCL gathers into the row views (uneven
+    all-gather); gloo, which has no uneven all-gather, through a padded buffer.
+A hidden layer's aggregation writes its output rows straight into the rank's
+block of the next exchange's ``[rows, 72]`` table (output row stride 72), the
+next layer's s of those rows lands in columns 64..71, and after the in-place
+all-gather the next layer reads h = table[:, :64] and s = table[:, 64:72] as
+strided views.
 """
 from __future__ import annotations
 
@@ -89,16 +105,80 @@ class ShardSpec:
         self.dst_lo, self.dst_hi = self.dst_bounds[rank], self.dst_bounds[rank + 1]
         self.node_lo, self.node_hi = self.node_bounds[rank], self.node_bounds[rank + 1]
 
+    def equal_blocks(self) -> bool:
+        """Rank r's destinations start at r * per (the node-balanced layout)."""
+        return all(self.dst_bounds[r] == r * self.per for r in range(self.world))
+
     def __repr__(self) -> str:
         return (f"ShardSpec(rank={self.rank}/{self.world}, dst=[{self.dst_lo},{self.dst_hi}), "
                 f"nodes=[{self.node_lo},{self.node_hi}))")
 
 
-def all_gather_v_rows(local: torch.Tensor, bounds: List[int], group=None) -> torch.Tensor:
-    """All-gather uneven row blocks (``bounds[r]:bounds[r+1]`` from rank r).
+class LogitsTable:
+    """The attention logits a shard's aggregation reads (gfd_gat_aggregate_split):
+    ``s`` -- source logits of every node, a ``[rows >= N, >= 8]`` view (row =
+    node id, any row stride); ``t`` -- destination logits of the rank's own
+    destinations, a ``[n_dst, >= 8]`` view (local rows)."""
 
-    RCCL's all-gather wants equal blocks, so each block is zero-padded to the
-    largest one, gathered in one collective and the padding dropped."""
+    def __init__(self, s: torch.Tensor, t: torch.Tensor):
+        self.s, self.t = s, t
+
+    @classmethod
+    def from_st(cls, st: torch.Tensor, spec: "ShardSpec") -> "LogitsTable":
+        """Views of an ``[N, 16]`` (s | t) table: no copies."""
+        return cls(st[:, :8], st[spec.dst_lo:spec.dst_hi, 8:])
+
+    def st(self, spec: "ShardSpec") -> torch.Tensor:
+        """An ``[N, 16]`` table (t rows set for the own destinations only): tests."""
+        n = spec.num_nodes
+        out = torch.zeros((n, 16), dtype=self.s.dtype, device=self.s.device)
+        out[:, :8] = self.s[:n, :8]
+        out[spec.dst_lo:spec.dst_hi, 8:] = self.t[:, :8]
+        return out
+
+
+def exchange_table(cols: int, spec: ShardSpec, device, dtype=torch.float32) -> torch.Tensor:
+    """An exchange table laid out by ``spec`` (module docstring): rows
+    ``world * per`` for equal blocks, else N."""
+    rows = spec.world * spec.per if spec.equal_blocks() else spec.num_nodes
+    return torch.empty((max(rows, spec.num_nodes, 1), cols), dtype=dtype, device=device)
+
+
+def own_block(table: torch.Tensor, spec: ShardSpec) -> torch.Tensor:
+    """The rank's rows of an exchange table (its destinations, in order)."""
+    return table[spec.dst_lo:spec.dst_hi]
+
+
+def gather_blocks(table: torch.Tensor, spec: ShardSpec, group=None) -> None:
+    """All-gather every rank's block of ``table`` in place (each rank has
+    written its own block; every row of the table is then valid).  Equal
+    blocks: one ``all_gather_into_tensor`` over the ``[world * per]`` rows.
+    Uneven: RCCL's uneven all-gather into the row views, or for gloo (no
+    uneven all-gather) a padded buffer copied out."""
+    if spec.world == 1:
+        return
+    import torch.distributed as dist
+    b, per, w = spec.dst_bounds, spec.per, spec.world
+    if spec.equal_blocks():
+        dist.all_gather_into_tensor(table[:w * per], table[spec.rank * per:(spec.rank + 1) * per],
+                                    group=group)
+        return
+    views = [table[b[r]:b[r + 1]] for r in range(w)]
+    if dist.get_backend(group) != "gloo":
+        dist.all_gather(views, views[spec.rank], group=group)
+        return
+    buf = table.new_zeros((per * w,) + tuple(table.shape[1:]))
+    mine = buf[spec.rank * per:spec.rank * per + views[spec.rank].shape[0]]
+    mine.copy_(views[spec.rank])
+    dist.all_gather_into_tensor(buf, buf[spec.rank * per:(spec.rank + 1) * per].clone(),
+                                group=group)
+    for r in range(w):
+        views[r].copy_(buf[r * per:r * per + views[r].shape[0]])
+
+
+def all_gather_v_rows(local: torch.Tensor, bounds: List[int], group=None) -> torch.Tensor:
+    """All-gather uneven row blocks (``bounds[r]:bounds[r+1]`` from rank r) into
+    a new ``[N, cols]`` tensor (the model's final outputs)."""
     import torch.distributed as dist
     world = len(bounds) - 1
     sizes = [bounds[r + 1] - bounds[r] for r in range(world)]
@@ -140,8 +220,8 @@ def shard_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
 def logits_rows(x: torch.Tensor, packed: torch.Tensor, lo: int, hi: int,
                 xmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``[hi - lo, 16]`` attention logits (s | t) of rows lo:hi of x
-    (gfd_gat_logits_ex); ``xmax`` (optional one-float device tensor)
-    accumulates max |x| over those rows (atomic max)."""
+    (gfd_gat_logits_ex, any row stride); ``xmax`` (optional one-float device
+    tensor) accumulates max |x| over those rows (atomic max)."""
     from . import _lib
     from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
     H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
@@ -155,14 +235,12 @@ def logits_rows(x: torch.Tensor, packed: torch.Tensor, lo: int, hi: int,
 
 def exchange_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
                     xmax: Optional[torch.Tensor] = None, group=None,
-                    logits_fn=None) -> torch.Tensor:
-    """The ``[N, 16]`` logits table a shard's aggregation reads: s (columns
-    0..7) for every node, t (8..15) for the rank's destinations
-    ``dst_lo:dst_hi`` (other rows' t are never read and left unset).
-
-    ONE logits pass per rank, over its own destination block (the only rows
-    whose t it reads), then one RCCL all-gather-v of the s half (``[N, 8]``:
-    half the bytes of gathering [s | t]; blocks padded to the largest).
+                    logits_fn=None) -> LogitsTable:
+    """The logits a shard's aggregation reads: s of every node, t of the rank's
+    destinations.  ONE logits pass per rank over its own destination block
+    (the only rows whose t it reads), its s rows written into its block of an
+    ``[rows, 8]`` exchange table, then one in-place all-gather of that table
+    (``gather_blocks``: 32 B per node; half the bytes of gathering [s | t]).
     ``logits_fn(lo, hi)`` -> [hi - lo, 16] replaces the HIP logits (tests)."""
     H = 8
     N = x.size(0)
@@ -170,44 +248,61 @@ def exchange_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
         def logits_fn(lo, hi):
             return logits_rows(x, packed, lo, hi, xmax)
     if spec.world == 1:
-        return logits_fn(0, N)
+        st = logits_fn(0, N)
+        return LogitsTable(st[:, :H], st[:, H:])
     blk = logits_fn(spec.dst_lo, spec.dst_hi)
-    s_all = all_gather_v_rows(blk[:, :H], spec.dst_bounds, group=group)
-    st = torch.empty((N, 2 * H), dtype=torch.float32, device=blk.device)
-    st[:, :H] = s_all
-    if spec.dst_hi > spec.dst_lo:
-        st[spec.dst_lo:spec.dst_hi, H:] = blk[:, H:]
-    return st
+    s_tab = exchange_table(H, spec, blk.device)
+    own_block(s_tab, spec).copy_(blk[:, :H])
+    gather_blocks(s_tab, spec, group)
+    return LogitsTable(s_tab, blk[:, H:])
 
 
-def shard_aggregate(x: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tensor,
-                    bias: Optional[torch.Tensor], spec: ShardSpec,
-                    negative_slope: float = 0.2,
-                    xmax: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``[dst_hi - dst_lo, 64]`` outputs of this rank's destinations, given the
-    all-gathered ``[N, 16]`` logits (gfd_gat_aggregate_ex, hubs + tiles); with
-    ``xmax`` = max |x| over all rows the tile stage uses one Z-row scale."""
+def _aggregate(h, graph, table: LogitsTable, packed, bias, spec, negative_slope, xmax, ep, out):
     from . import _lib
     from .graph import _ws
     from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
     lib = _lib.load()
     H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
-    N, F = x.shape
+    N, F = h.shape
     n_dst = spec.dst_hi - spec.dst_lo
-    out = torch.empty((n_dst, C), dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((n_dst, C), dtype=torch.float32, device=h.device)
+    if out.shape != (n_dst, C) or out.stride(1) != 1:
+        raise ValueError(f"out must be a [{n_dst}, {C}] view with unit column stride")
     if n_dst == 0:
         return out
+    s, t = table.s, table.t
+    if s.stride(1) != 1 or t.stride(1) != 1 or s.size(0) < N or t.size(0) < n_dst:
+        raise ValueError("logits table: s [>= N, 8] and t [>= n_dst, 8] row views")
     shard = graph.shard(spec.dst_lo, spec.dst_hi)   # plan built once per range, cached
     plan = shard.plan
     ws = _ws(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, plan.num_hubs, plan.num_chunks),
-             x.device)
-    _lib.call("gfd_gat_aggregate_ex", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
-              shard.rowptr.data_ptr(),
-              graph.col.data_ptr(), n_dst, spec.dst_lo, st.data_ptr(), _lib.ptr(xmax),
-              packed.data_ptr(),
-              _lib.ptr(bias), H, C, float(negative_slope), 0.0, 0, plan.cstruct(),
-              3, out.data_ptr(), None, ws.data_ptr(), ws.numel(), _lib.stream_handle(x.device))
+             h.device)
+    _lib.call("gfd_gat_aggregate_split", h.data_ptr(), _lib.x_dtype_code(h), N, F, h.stride(0),
+              shard.rowptr.data_ptr(), graph.col.data_ptr(), n_dst, spec.dst_lo, s.data_ptr(),
+              s.stride(0), t.data_ptr(), t.stride(0), _lib.ptr(xmax), packed.data_ptr(),
+              _lib.ptr(bias), H, C, float(negative_slope), 0.0, 0, plan.cstruct(), 3,
+              _lib.ct.byref(ep) if ep is not None else None, out.data_ptr(), out.stride(0), None,
+              ws.data_ptr(), ws.numel(), _lib.stream_handle(h.device))
     return out
+
+
+def _as_table(st, spec) -> LogitsTable:
+    return st if isinstance(st, LogitsTable) else LogitsTable.from_st(st, spec)
+
+
+def shard_aggregate(x: torch.Tensor, graph, st, packed: torch.Tensor,
+                    bias: Optional[torch.Tensor], spec: ShardSpec,
+                    negative_slope: float = 0.2,
+                    xmax: Optional[torch.Tensor] = None,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``[dst_hi - dst_lo, 64]`` outputs of this rank's destinations
+    (gfd_gat_aggregate_split, hubs + tiles) given the logits (a LogitsTable,
+    or an ``[N, 16]`` s | t table); with ``xmax`` = max |x| over all rows the
+    tile stage uses one Z-row scale.  ``out``: an ``[n_dst, 64]`` view (any row
+    stride) to write into -- the rank's block of the next exchange table."""
+    return _aggregate(x, graph, _as_table(st, spec), packed, bias, spec, negative_slope, xmax,
+                      None, out)
 
 
 def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torch.Tensor,
@@ -218,73 +313,67 @@ def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torc
 
     ``x`` is halo-resident (all N rows on every rank, row stride may be
     padded), ``graph`` the full CSR.  Steps: pack weights -> ``exchange_logits``
-    (one RCCL all-gather of the SOURCE logits ``[N, 8]``; t recomputed for the
-    rank's own destinations) and max|x| reduced -> fused aggregate-project over
-    the rank's destinations -> (optionally) all-gather-v of the ``[n_dst, 64]``
-    outputs.
+    (the own block's logits, one in-place all-gather of the SOURCE logits
+    ``[N, 8]``) and max|x| reduced -> fused aggregate-project over the rank's
+    destinations -> (optionally) all-gather of the ``[n_dst, 64]`` outputs.
     """
     if x.stride(1) != 1:
         raise ValueError("x rows must be contiguous")
     packed = pack_weights(weight, att_src, att_dst)
     xmax = torch.zeros(1, dtype=torch.float32, device=x.device)
-    st = exchange_logits(x, packed, spec, xmax, group=group)
+    table = exchange_logits(x, packed, spec, xmax, group=group)
     if spec.world > 1:
         import torch.distributed as dist
         dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
-    out = shard_aggregate(x, graph, st, packed, bias, spec, negative_slope, xmax)
-    if gather_output:
-        return all_gather_v_rows(out, spec.dst_bounds, group=group)
-    return out
+    if not gather_output or spec.world == 1:
+        return shard_aggregate(x, graph, table, packed, bias, spec, negative_slope, xmax)
+    full = exchange_table(64, spec, x.device)
+    shard_aggregate(x, graph, table, packed, bias, spec, negative_slope, xmax,
+                    out=own_block(full, spec))
+    gather_blocks(full, spec, group)
+    return full[:spec.num_nodes]
 
 
 # ---------------------------------------------------------------------------
 # Model-level sharding: every layer of the reference stack (gat.py:79-94,
 # tgn.py:93-111) destination-sharded, eval mode.
 
-def shard_aggregate_ep(h: torch.Tensor, graph, st: torch.Tensor, packed: torch.Tensor,
+HID = 72   # hidden exchange row: h (64) | next layer's s (8)
+
+
+def shard_aggregate_ep(h: torch.Tensor, graph, st, packed: torch.Tensor,
                        bias: Optional[torch.Tensor], spec: ShardSpec, negative_slope: float,
                        xmax: Optional[torch.Tensor], scale_shift: torch.Tensor, relu: bool,
-                       residual: Optional[torch.Tensor]) -> torch.Tensor:
+                       residual: Optional[torch.Tensor],
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """shard_aggregate with the layer body's inference epilogue fused into the
-    output store (gfd_gat_aggregate_ep): BN(eval) affine, ReLU, residual rows
-    (``residual`` = the layer input rows of this shard's destinations)."""
+    output store (BN(eval) affine, ReLU, residual rows: ``residual`` = the
+    layer input rows of this shard's destinations, any row stride).  ``out``
+    as shard_aggregate (the rank's block of the next exchange table)."""
     from . import _lib
-    from .graph import _ws
-    from .nn import SUPPORTED_CHANNELS, SUPPORTED_HEADS
-    lib = _lib.load()
-    H, C = SUPPORTED_HEADS, SUPPORTED_CHANNELS
-    N, F = h.shape
-    n_dst = spec.dst_hi - spec.dst_lo
-    out = torch.empty((n_dst, C), dtype=torch.float32, device=h.device)
-    if n_dst == 0:
-        return out
-    shard = graph.shard(spec.dst_lo, spec.dst_hi)
-    plan = shard.plan
-    ws = _ws(lib.gfd_gat_fwd_workspace_size(N, n_dst, F, H, C, plan.num_hubs, plan.num_chunks),
-             h.device)
     ep = _lib.GfdEpilogue(scale_shift.data_ptr(), 1 if relu else 0, _lib.ptr(residual),
                           residual.stride(0) if residual is not None else 0)
-    _lib.call("gfd_gat_aggregate_ep", h.data_ptr(), _lib.x_dtype_code(h), N, F, h.stride(0),
-              shard.rowptr.data_ptr(), graph.col.data_ptr(), n_dst, spec.dst_lo, st.data_ptr(),
-              _lib.ptr(xmax), packed.data_ptr(), _lib.ptr(bias), H, C, float(negative_slope), 0.0,
-              0, plan.cstruct(), 3, _lib.ct.byref(ep), out.data_ptr(), None, ws.data_ptr(),
-              ws.numel(), _lib.stream_handle(h.device))
-    return out
+    return _aggregate(h, graph, _as_table(st, spec), packed, bias, spec, negative_slope, xmax,
+                      ep, out)
 
 
 def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, residual: bool,
-                          group=None, st: Optional[torch.Tensor] = None,
-                          xmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+                          group=None, st=None, xmax: Optional[torch.Tensor] = None,
+                          packed: Optional[torch.Tensor] = None,
+                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One layer body on this rank: source logits exchanged
     (``exchange_logits``) and max|x| reduced, the rank's destinations
     aggregated with BN / ReLU / residual in the store.  ``h`` is the layer
-    input for ALL N nodes (layer 0: the halo-resident features).  ``st`` /
-    ``xmax``: the logits table and max |h| when the caller already has them
-    (hidden layers: they arrive with the all-gathered rows)."""
+    input for ALL N nodes (layer 0: the halo-resident features; hidden layers:
+    the gathered table's view).  ``st`` / ``xmax`` / ``packed``: the logits
+    table, max |h| and the packed weights when the caller already has them
+    (hidden layers: they come with the gathered rows).  ``out``: where the
+    output rows go (the rank's block of the next exchange table)."""
     import torch.distributed as dist
     from .fused import bn_affine
-    packed = pack_weights(conv.lin_src.weight.detach(), conv.att_src.detach(),
-                          conv.att_dst.detach())
+    if packed is None:
+        packed = pack_weights(conv.lin_src.weight.detach(), conv.att_src.detach(),
+                              conv.att_dst.detach())
     if st is None:
         xmax = torch.zeros(1, dtype=torch.float32, device=h.device)
         st = exchange_logits(h, packed, spec, xmax, group=group)
@@ -296,45 +385,34 @@ def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, res
         res = res if res.dtype == torch.float32 else res.float()
     bias = conv.bias.detach() if conv.bias is not None else None
     return shard_aggregate_ep(h, graph, st, packed, bias, spec, conv.negative_slope, xmax,
-                              bn_affine(bn, h.device), True, res)
+                              bn_affine(bn, h.device), True, res, out=out)
 
 
-def gather_hidden(out_local: torch.Tensor, next_conv, spec: ShardSpec, group=None):
-    """The exchange before a hidden layer, as ONE collective: every rank
-    computes the next layer's logits [s | t] of its own output rows (they are
-    local), then all-gathers ``[out | s | max|out|]`` rows (all-gather-v,
-    72 columns).  Returns (h [N, 64] view with row stride 72, the [N, 16]
-    logits table -- s for every node, t for this rank's destinations -- and
-    max |h| over all rows, reduced over ranks by the same collective)."""
+def gather_hidden(table: torch.Tensor, next_conv, spec: ShardSpec, group=None):
+    """The exchange before a hidden layer, copy-free.  ``table`` is the
+    ``[rows, 72]`` exchange table whose own block's columns 0..63 already hold
+    this rank's output rows (the aggregation wrote them there).  The rank
+    computes the next layer's logits of those rows (they are local), writes
+    their s into columns 64..71 of its block, and ONE in-place all-gather
+    fills every block; max |h| is reduced alongside.  Returns (h: [N, 64] view
+    of the table, row stride 72; the LogitsTable: s = [N, 8] view of the
+    table, t = this rank's destinations; max |h|; the packed weights)."""
+    import torch.distributed as dist
     H, C = 8, 64
-    n_dst = out_local.size(0)
-    dev = out_local.device
+    dev = table.device
     packed = pack_weights(next_conv.lin_src.weight.detach(), next_conv.att_src.detach(),
                           next_conv.att_dst.detach())
-    xmax_l = torch.zeros(1, dtype=torch.float32, device=dev)
-    st_l = logits_rows(out_local, packed, 0, n_dst, xmax_l)
-    rows = torch.empty((n_dst, C + H), dtype=torch.float32, device=dev)
-    rows[:, :C] = out_local
-    rows[:, C:] = st_l[:, :H]
-    # max |h| travels in an extra column of each rank's first row block: the
-    # padded row 0 of every block (all_gather_v pads to the largest block)
-    world = spec.world
-    sizes = [spec.dst_bounds[r + 1] - spec.dst_bounds[r] for r in range(world)]
-    per = max(max(sizes), 1) + 1
-    import torch.distributed as dist
-    buf = rows.new_zeros((per, C + H))
-    buf[0, 0] = xmax_l[0]
+    mine = own_block(table, spec)
+    n_dst = mine.size(0)
+    xmax = torch.zeros(1, dtype=torch.float32, device=dev)
+    st_l = logits_rows(mine[:, :C], packed, 0, n_dst, xmax)
     if n_dst:
-        buf[1:1 + n_dst] = rows
-    allb = rows.new_empty((per * world, C + H))
-    dist.all_gather_into_tensor(allb, buf, group=group)
-    xmax = allb[0::per, 0].max().reshape(1).contiguous()
-    full = torch.cat([allb[r * per + 1:r * per + 1 + sizes[r]] for r in range(world)])
-    st = torch.empty((full.size(0), 2 * H), dtype=torch.float32, device=dev)
-    st[:, :H] = full[:, C:]
-    if n_dst:
-        st[spec.dst_lo:spec.dst_hi, H:] = st_l[:, H:]
-    return full[:, :C], st, xmax
+        mine[:, C:] = st_l[:, :H]
+    gather_blocks(table, spec, group)
+    if spec.world > 1:
+        dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
+    n = spec.num_nodes
+    return table[:n, :C], LogitsTable(table[:n, C:], st_l[:, H:]), xmax, packed
 
 
 def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=None,
@@ -343,29 +421,29 @@ def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=
     reference's 2-3 layer stacks, gat.py:60-96, tgn.py:67-113) on this rank.
 
     Layer 0 reads the halo-resident features (all N rows on every rank; the
-    exchange is the [N, 8] source-logits all-gather).  Before each layer >= 1
-    ONE collective (``gather_hidden``) moves the previous layer's output rows
-    together with the next layer's source logits, computed by the row's owner
-    (72 columns: 2.9 GB in total at C4) -- the logits exchange rides along
-    instead of costing a second collective.  The heads (Linear, GRUCell +
-    Linear) are row-local.  Returns the outputs of the rank's destinations, or
-    of all N nodes (gather_output).  Inference only."""
+    exchange is the [N, 8] source-logits all-gather).  Every hidden layer's
+    aggregation writes its rows straight into the rank's block of a ``[rows,
+    72]`` exchange table, and ONE in-place collective (``gather_hidden``) moves
+    them together with the next layer's source logits (computed by the row's
+    owner): 2.9 GB in total at C4, no copies on either side of it.  The heads
+    (Linear, GRUCell + Linear) are row-local.  Returns the outputs of the
+    rank's destinations, or of all N nodes (gather_output).  Inference only."""
     if model.training or torch.is_grad_enabled():
         raise RuntimeError("model_forward_sharded is inference-only: model.eval() and no_grad")
     h = x
     L = len(model.gat_layers)
-    st = xmax = None
+    st = xmax = packed = None
     for layer, conv in enumerate(model.gat_layers):
         bn = model.batch_norms[layer] if model.batch_norms is not None else None
         res = model.residual and h.size(-1) == model.hidden_channels
-        out_local = layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax)
-        if layer < L - 1:
-            if spec.world > 1:
-                h, st, xmax = gather_hidden(out_local, model.gat_layers[layer + 1], spec, group)
-            else:
-                h, st, xmax = out_local, None, None
+        if layer < L - 1 and spec.world > 1:
+            table = exchange_table(HID, spec, x.device)
+            layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed,
+                                  out=own_block(table, spec)[:, :64])
+            h, st, xmax, packed = gather_hidden(table, model.gat_layers[layer + 1], spec, group)
         else:
-            h = out_local
+            h = layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed)
+            st = xmax = packed = None
     if hasattr(model, "gru"):
         from .fused import gru_head
         out, hid = gru_head(model.gru, model.out, h)

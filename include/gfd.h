@@ -411,8 +411,10 @@ gfd_status gfd_gat_aggregate_ep(const void* x, int x_dtype, int64_t num_nodes, i
  * table between the collective and the kernels).
  *   s_log [num_nodes rows, s_stride >= H]: s_j of every node (global rows);
  *   t_log [num_dst rows, t_stride >= H]: t_i of destination dst_offset + i.
+ * out row i (destination dst_offset + i) at out + i * out_stride (>= C): a
+ * rank writes its rows straight into its block of the next exchange's table.
  * gfd_gat_aggregate_ep(st) equals this with s_log = st, t_log = st +
- * 16 dst_offset + H, both strides 16.  Replaces the same PyG GATConv.forward
+ * 16 dst_offset + H, both strides 16, out_stride C.  Replaces the same PyG GATConv.forward
  * steps as gfd_gat_aggregate_ex (gat.py:80). */
 gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t num_nodes,
                                    int in_features, int64_t x_stride, const int32_t* rowptr,
@@ -422,11 +424,11 @@ gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t num_nodes
                                    const float* bias, int heads, int channels,
                                    float negative_slope, float dropout_p, uint64_t dropout_seed,
                                    const gfd_plan* plan, int stages, const gfd_epilogue* ep,
-                                   float* out, float* stats, void* ws, size_t ws_bytes,
-                                   gfd_stream_t stream);
+                                   float* out, int64_t out_stride, float* stats, void* ws,
+                                   size_t ws_bytes, gfd_stream_t stream);
 
 /* gfd_gat_logits_lone writing s (row i at s_log + i s_stride) and t (t_log +
- * i t_stride) separately: a rank's own destination block writes its s rows
+ * i t_stride) separately, lone output rows at out + i out_stride: a rank's own destination block writes its s rows
  * straight into its slot of the all-gathered [N, H] s table.  Replaces the
  * same PyG GATConv.forward steps as gfd_gat_logits_lone. */
 gfd_status gfd_gat_logits_lone_split(const void* x, int x_dtype, int64_t num_nodes,
@@ -434,7 +436,8 @@ gfd_status gfd_gat_logits_lone_split(const void* x, int x_dtype, int64_t num_nod
                                      int heads, int channels, const int32_t* rowptr,
                                      const float* bias, float negative_slope, float* s_log,
                                      int64_t s_stride, float* t_log, int64_t t_stride,
-                                     float* xmax, float* out, float* stats, gfd_stream_t stream);
+                                     float* xmax, float* out, int64_t out_stride, float* stats,
+                                     gfd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * GATConv backward (autograd of the PyG dataflow at loss.backward(),

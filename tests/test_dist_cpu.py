@@ -67,7 +67,7 @@ def _rank_main(rank, world, port, q):
         st = gdist.all_gather_rows(st_local, N, world)
         # the product exchange: s of every node gathered, [s | t] of the own destinations
         st_x = gdist.exchange_logits(x, None, spec,
-                                     logits_fn=lambda lo, hi: _logits(x[lo:hi], W, a_s, a_d))
+                                     logits_fn=lambda lo, hi: _logits(x[lo:hi], W, a_s, a_d)).st(spec)
         out_local = ref.gatconv_forward_at(x, rowptr, col, torch.arange(spec.dst_lo, spec.dst_hi),
                                            W, a_s, a_d, b)
         out = gdist.all_gather_v_rows(out_local, spec.dst_bounds)

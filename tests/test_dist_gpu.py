@@ -82,3 +82,47 @@ def test_rccl_world1_end_to_end():
     finally:
         dist.destroy_process_group()
     assert_close(out, ref.gatconv_forward(x, ei, W, a_s, a_d, b, heads=H), what="RCCL world 1")
+
+
+@pytest.mark.parametrize("balance", ["nodes", "messages"])
+def test_exchange_tables_are_read_and_written_in_place(balance):
+    """The hidden-layer exchange layout (gfd.dist.gather_hidden): a layer's
+    input h and the next layer's s read as strided views of one [rows, 72]
+    table, t from the own block's logits (stride 16), residual rows from the
+    same view, and the aggregation writing its output rows straight into the
+    rank's block of the next table (output row stride 72).  Every rank's rows
+    must equal the contiguous-tensor call bit for bit, and the table's other
+    columns must be left alone."""
+    from gfd import dist as gdist, graph as ggraph
+    from gfd.fused import bn_affine
+    dev = torch.device("cuda", 0)
+    N, E, F, world = 6000, 48000, 64, 3
+    ei, x, W, a_s, a_d, b = _problem(N, E, F, 13, dev)
+    g = ggraph.csr_from_coo(ei.to(dev), N)
+    W, a_s, a_d, b = W.to(dev), a_s.to(dev), a_d.to(dev), b.to(dev)
+    packed = gdist.pack_weights(W, a_s, a_d)
+    bn = torch.nn.BatchNorm1d(64).to(dev).eval()
+    with torch.no_grad():
+        bn.running_mean.normal_()
+        bn.running_var.uniform_(0.5, 2.0)
+    aff = bn_affine(bn, dev)
+    h = x.to(dev)
+    st = gdist.logits_rows(h, packed, 0, N)
+    specs = [gdist.ShardSpec(g.rowptr, r, world, balance) for r in range(world)]
+    table = gdist.exchange_table(gdist.HID, specs[0], dev)
+    table.fill_(float("nan"))
+    table[:N, :64] = h
+    table[:N, 64:] = st[:, :8]
+    nxt = gdist.exchange_table(gdist.HID, specs[0], dev)
+    nxt.fill_(7.0)
+    for sp in specs:
+        lo, hi = sp.dst_lo, sp.dst_hi
+        want = gdist.shard_aggregate_ep(h, g, st, packed, b, sp, 0.2, None, aff, True, h[lo:hi])
+        hv = table[:N, :64]
+        tab = gdist.LogitsTable(table[:N, 64:], st[lo:hi, 8:])
+        got = gdist.shard_aggregate_ep(hv, g, tab, packed, b, sp, 0.2, None, aff, True, hv[lo:hi],
+                                       out=gdist.own_block(nxt, sp)[:, :64])
+        torch.cuda.synchronize()
+        assert got.data_ptr() == nxt[lo:].data_ptr()
+        assert torch.equal(got, want), f"rank {sp.rank}: strided tables differ"
+    assert torch.all(nxt[:N, 64:] == 7.0), "the s columns of the next table were written"

@@ -57,7 +57,14 @@ def _patch_oracle_stages(gdist, ei):
         return torch.cat([(hh * a_s).sum(-1), (hh * a_d).sum(-1)], 1)
 
     def shard_aggregate_ep(h, graph, st, packed, bias, spec, slope, xmax, scale_shift, relu,
-                           residual):
+                           residual, out=None):
+        # the logits table the product passes must hold every node's s and the
+        # own destinations' t (checked against a recomputation)
+        table = gdist._as_table(st, spec)
+        full = logits_rows(h, packed, 0, h.size(0))
+        assert torch.allclose(table.s[:h.size(0)], full[:, :H], atol=1e-5, rtol=1e-5)
+        assert torch.allclose(table.t[:spec.dst_hi - spec.dst_lo], full[spec.dst_lo:spec.dst_hi, H:],
+                              atol=1e-5, rtol=1e-5)
         rowptr, col = graph
         y = ref.gatconv_forward_at(h, rowptr, col, torch.arange(spec.dst_lo, spec.dst_hi),
                                    packed["W"], packed["a_s"].view(1, H, C),
@@ -65,7 +72,11 @@ def _patch_oracle_stages(gdist, ei):
         y = y * scale_shift[:C] + scale_shift[C:]
         if relu:
             y = torch.relu(y)
-        return y + residual if residual is not None else y
+        y = y + residual if residual is not None else y
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
 
     gdist.pack_weights = pack_weights
     gdist.logits_rows = logits_rows
@@ -86,7 +97,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, balance="messages"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "gnn-fraud-detection_amd")):
@@ -100,7 +111,7 @@ def _rank_main(rank, world, port, q):
         ei, x, m = _problem()
         _patch_oracle_stages(gdist, ei)
         rowptr, col = csr_cpu(ei, N)
-        spec = gdist.ShardSpec(rowptr, rank, world)
+        spec = gdist.ShardSpec(rowptr, rank, world, balance)
         with torch.no_grad():
             out = gdist.model_forward_sharded(m, x, (rowptr, col), spec)
         if rank == 0:
@@ -109,12 +120,16 @@ def _rank_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_model_sharded_orchestration_gloo(world):
+@pytest.mark.parametrize("world,balance", [(2, "messages"), (3, "messages"), (4, "messages"),
+                                           (3, "nodes"), (4, "nodes")])
+def test_model_sharded_orchestration_gloo(world, balance):
+    """balance "nodes": equal blocks, every exchange one in-place all-gather
+    into the layer's table; "messages": uneven blocks (gloo's padded path)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _store_path()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, balance))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = q.get(timeout=180)
