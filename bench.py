@@ -374,7 +374,15 @@ def cpu_baseline(s, args):
     tt = sorted(times[1:])
     med, mn = tt[len(tt) // 2], tt[0]
     in_edges = msgs - dsts.numel()   # input edges of the sample (each dst has one self loop)
+    # the whole C4 graph, projected from the sample (the dataflow's work is
+    # per message: gather, projection of the gathered rows, message tensor,
+    # scatter); BASELINE.md §4's dst-sorted chunked full run would take about
+    # this long per run, which does not fit beside the other legs' time limit
+    full_s = med * g.num_messages / msgs
     return {"value": in_edges / med, "unit": "edges/s", "cores": threads, "kind": "port",
+            "projected_full_graph_s": round(full_s, 1),
+            "projected_full_graph_note": f"median x messages ({g.num_messages}) / sampled "
+                                         f"messages ({msgs}): linear in messages",
             "min_s": round(mn, 3), "median_s": round(med, 3), "runs": args.cpu_runs,
             "cpu_model": cpu_model(), "value_best": in_edges / mn,
             "sample": f"{dsts.numel()} random destinations of the C4 graph itself "
