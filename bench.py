@@ -67,6 +67,9 @@ def parse(argv=None):
                    help="N > 1 ranks on however many GPUs are visible (rank -> GPU rank %% "
                         "count), gloo host-staged exchange: exercises the launcher and the "
                         "per-rank path on a 1-GPU box; NOT a scaling measurement")
+    p.add_argument("--no-s-in-row", action="store_true",
+                   help="keep the source logits in their own [N, 16] table instead of an "
+                        "8-float slot in every x row")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-legs", action="store_true")
     p.add_argument("--legs", default="c4bwd,sample,c5,c1,c2,c3,temporal,ingest",
@@ -86,11 +89,17 @@ def glorot(shape, gen, device):
 
 
 def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, world=1,
-          row_align=16, balance="nodes"):
+          row_align=16, balance="nodes", s_in_row=True):
     """The bench workload, built on the device exactly as timed: Chung-Lu
     graph (seed 1) -> CSR, x ~ N(0,1) (seed 0) at a 16-B row pitch, glorot W
     (seed 0), zero bias, this rank's destination shard and its cached plan.
-    Also used by tests/test_bench_parity_gpu.py."""
+    ``s_in_row``: every x row carries an 8-float slot for its node's source
+    logits s_j after the features (16-B aligned), written by the logits pass
+    and read by the gather kernels through gfd_gat_aggregate_split's (s,
+    s_stride) -- so a message's s_j comes from the line its x row's gather
+    fetches anyway instead of a line of its own (fp32 F = 166: pitch 176, the
+    slot at 168; bf16: pitch 184, the slot at 168).  The features x = xbuf[:, :F]
+    are unchanged.  Also used by tests/test_bench_parity_gpu.py."""
     from gfd import dist as gdist, graph as ggraph, synth
     ei = synth.power_law_device(nodes, edges, gamma=gamma, seed=1, device=dev)
     g = ggraph.csr_from_coo(ei, nodes)
@@ -100,7 +109,9 @@ def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, worl
     esz = torch.tensor([], dtype=dtype).element_size()
     # rows aligned to row_align bytes: 16 -> pitch 168 for F = 166; 128 -> whole
     # 128-B lines per row (pitch 192: fp32 6 lines, bf16 3 lines per gathered row)
-    ldx = (F * esz + row_align - 1) // row_align * row_align // esz
+    s_off = (F * esz + 15) // 16 * 16                      # byte offset of the s slot
+    row_bytes = s_off + 4 * H if s_in_row else F * esz
+    ldx = (row_bytes + row_align - 1) // row_align * row_align // esz
     xbuf = torch.randn((nodes, ldx), generator=gx, device=dev, dtype=torch.float32).to(dtype)
     x = xbuf[:, :F]
     gen = torch.Generator().manual_seed(0)
@@ -111,7 +122,9 @@ def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, worl
     spec = gdist.ShardSpec(g.rowptr, rank, world, balance)   # the rank's destinations
     shard = g.shard(spec.dst_lo, spec.dst_hi)
     return {"graph": g, "x": x, "xbuf": xbuf, "ldx": ldx, "W": W, "a_s": a_s, "a_d": a_d,
-            "bias": bias, "spec": spec, "shard": shard, "dtype": dtype, "F": F}
+            "bias": bias, "spec": spec, "shard": shard, "dtype": dtype, "F": F,
+            # the s slot as a float pointer offset and float row stride (or None)
+            "s_row": (s_off // 4, ldx * esz // 4) if s_in_row else None}
 
 
 class Layer:
@@ -157,6 +170,20 @@ class Layer:
         # skips that class -- whole graph or shard, at every world size
         self.whole = spec.dst_lo == 0 and spec.dst_hi == self.N and world == 1
         self.stages = self.STAGES_FUSED if world == 1 else self.STAGES_SHARDED
+        # whole graph with an s slot in every x row: s written into the rows by
+        # the logits pass, t into t_loc, both read through the split ABI
+        self.in_row = self.whole and s.get("s_row") is not None
+        if self.in_row:
+            off, self.lds = s["s_row"]
+            self.s_ptr = s["xbuf"].data_ptr() + 4 * off
+
+    def logits_table(self):
+        """[N, 16] s | t of the last step (tests): from the row slots or st."""
+        if not self.in_row:
+            return self.st
+        off, lds = self.s["s_row"]
+        rows = self.s["xbuf"].view(torch.float32).view(self.N, lds)   # bf16 rows: as bytes
+        return torch.cat([rows[:, off:off + H], self.t_loc[:self.N]], 1)
 
     def pack_and_logits(self):
         s, _lib, F = self.s, self._lib, self.s["F"]
@@ -164,6 +191,12 @@ class Layer:
                   s["a_d"].data_ptr(), F, H, C, self.packed.data_ptr(), self.stream)
         self.xmax.zero_()
         x, spec = s["x"], s["spec"]
+        if self.in_row:
+            _lib.call("gfd_gat_logits_lone_split", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
+                      self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
+                      s["bias"].data_ptr(), 0.2, self.s_ptr, self.lds, self.t_loc.data_ptr(), H,
+                      self.xmax.data_ptr(), self.out.data_ptr(), C, None, self.stream)
+            return
         if self.whole:
             _lib.call("gfd_gat_logits_lone", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
                       self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
@@ -214,6 +247,14 @@ class Layer:
 
     def aggregate(self, stages):
         s = self.s
+        if self.in_row:
+            self._lib.call("gfd_gat_aggregate_split", s["x"].data_ptr(), self.xdt, self.N, s["F"],
+                           s["ldx"], s["shard"].rowptr.data_ptr(), s["graph"].col.data_ptr(),
+                           self.n_dst, 0, self.s_ptr, self.lds, self.t_loc.data_ptr(), H,
+                           self.xmax.data_ptr(), self.packed.data_ptr(), s["bias"].data_ptr(), H,
+                           C, 0.2, 0.0, 0, self.cplan, stages, None, self.out.data_ptr(), C, None,
+                           self.ws.data_ptr(), self.ws.numel(), self.stream)
+            return
         if self.whole:
             self._lib.call("gfd_gat_aggregate_ex", s["x"].data_ptr(), self.xdt, self.N, s["F"],
                            s["ldx"], s["shard"].rowptr.data_ptr(), s["graph"].col.data_ptr(),
@@ -401,7 +442,7 @@ def measure(args, dev, rank, world, config):
         N, E, dtype = args.nodes or 10_000_000, args.edges or 50_000_000, torch.float32
     t_setup = time.perf_counter()
     s = setup(dev, N, E, F, args.gamma, dtype, rank, world, row_align=args.row_align,
-              balance=args.balance)
+              balance=args.balance, s_in_row=not args.no_s_in_row)
     layer = Layer(s, dev, world)
     plan = layer.plan
     esz = s["xbuf"].element_size()

@@ -40,7 +40,7 @@ def main():
     s = bench.setup(dev, a.nodes, a.edges, 166)
     whole = bench.Layer(s, dev, 1)
     el, whole_ms, _ = bench.time_layer(whole, a.steps, a.warmup, 1)
-    st_full, xmax = whole.st.clone(), whole.xmax.clone()
+    st_full, xmax = whole.logits_table().clone(), whole.xmax.clone()
     g = s["graph"]
 
     def all_gather_into_tensor(out, inp, group=None):

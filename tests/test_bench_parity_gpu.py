@@ -123,7 +123,7 @@ def test_bench_multi_rank_path(world, balance, monkeypatch):
     whole = bench.Layer(s, DEV, 1)
     whole.step()
     torch.cuda.synchronize()
-    ref, st_full, xmax = whole.out.clone(), whole.st.clone(), whole.xmax.clone()
+    ref, st_full, xmax = whole.out.clone(), whole.logits_table().clone(), whole.xmax.clone()
     spec0 = gdist.ShardSpec(g.rowptr, 0, world, balance)
     bounds, per = spec0.dst_bounds, spec0.per
     sent = []
