@@ -174,6 +174,16 @@ class _GRUHeadTrain(torch.autograd.Function):
                 g_bhh if b_hh is not None else None, g_wo, g_bo if b_o is not None else None)
 
 
+def _aligned_rows(t: torch.Tensor) -> torch.Tensor:
+    """t itself when its rows are unit-stride, 16-B aligned and at a 16-B
+    multiple pitch (what gfd_gru_head / _bwd read as vectors); otherwise a
+    fresh contiguous copy -- also for a contiguous view at a misaligned offset,
+    which .contiguous() would return unchanged."""
+    if t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0:
+        return t
+    return t.clone(memory_format=torch.contiguous_format)
+
+
 def tgn_head_train(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,
                    h0: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Training form of ``gru_head``: (lin(GRUCell(h, h0)), GRUCell(h, h0)) as
@@ -181,13 +191,9 @@ def tgn_head_train(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,
     (tgn.py:108-111 under loss.backward(), train.py:142)."""
     if gru.hidden_size != C or gru.input_size != C or not gru.bias:
         raise NotImplementedError("gfd tgn_head_train: GRUCell(64, 64) with biases")
-    x = h if h.dtype == torch.float32 else h.float()
-    x = x if x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 \
-        else x.contiguous()
+    x = _aligned_rows(h if h.dtype == torch.float32 else h.float())
     if h0 is not None:
-        h0 = h0.float() if h0.dtype != torch.float32 else h0
-        h0 = h0 if h0.stride(1) == 1 and h0.stride(0) % 4 == 0 and h0.data_ptr() % 16 == 0 \
-            else h0.contiguous()
+        h0 = _aligned_rows(h0.float() if h0.dtype != torch.float32 else h0)
     b_o = lin.bias
     return _GRUHeadTrain.apply(x, h0, gru.weight_ih.contiguous(), gru.bias_ih,
                                gru.weight_hh.contiguous(), gru.bias_hh, lin.weight.contiguous(),

@@ -254,7 +254,7 @@ _LOCK = threading.Lock()
 _BY_ID: dict = {}                      # id(edge_index) -> (weakref, key, graph)
 _BY_FP: "OrderedDict" = OrderedDict()  # (device, N, shape, fingerprint) -> graph
 _FP_CAP = 8                            # graphs held by content ...
-_FP_CAP_BYTES = 4 << 30                # ... and at most this many CSR bytes (LRU)
+_FP_CAP_BYTES = 4 << 30                # ... and at most this many device bytes (LRU)
 # Edge lists that skip the content cache: per-batch subgraphs of the sampler
 # (gfd.sampler.NeighborLoader marks them) are used once, and would otherwise
 # flood the cache and pay a fingerprint sync each.
@@ -276,8 +276,29 @@ def _single_use(edge_index: torch.Tensor) -> bool:
     return r is not None and r() is edge_index
 
 
+def _tensor_bytes(obj, depth: int = 0) -> int:
+    """Device bytes of the tensors an object holds (its attributes, tuples,
+    dicts; a few levels deep): a cached graph's CSR, lazily built CSC, plans and
+    shard plans."""
+    if isinstance(obj, torch.Tensor):
+        return obj.numel() * obj.element_size()
+    if depth > 3 or obj is None or isinstance(obj, (int, float, str, bool)):
+        return 0
+    if isinstance(obj, dict):
+        items = obj.values()
+    elif isinstance(obj, (tuple, list)):
+        items = obj
+    elif hasattr(obj, "__dict__"):
+        items = vars(obj).values()
+    else:
+        return 0
+    return sum(_tensor_bytes(v, depth + 1) for v in items)
+
+
 def _graph_bytes(g: "CSRGraph") -> int:
-    return g.rowptr.numel() * 4 + g.col.numel() * 4
+    """Everything the cached graph keeps on the device: rowptr + col and,
+    once built, its CSC, plan and per-range shard plans."""
+    return _tensor_bytes(g)
 
 
 def get_graph(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
@@ -307,10 +328,12 @@ def get_graph(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
         if fkey is not None:
             with _LOCK:
                 _BY_FP[fkey] = g
-                while len(_BY_FP) > 1 and (
-                        len(_BY_FP) > _FP_CAP or
-                        sum(_graph_bytes(v) for v in _BY_FP.values()) > _FP_CAP_BYTES):
-                    _BY_FP.popitem(last=False)
+                # sizes taken now (plans / CSC grow lazily after insertion);
+                # one sum, then a running total while evicting
+                total = sum(_graph_bytes(v) for v in _BY_FP.values())
+                while len(_BY_FP) > 1 and (len(_BY_FP) > _FP_CAP or total > _FP_CAP_BYTES):
+                    _, old = _BY_FP.popitem(last=False)
+                    total -= _graph_bytes(old)
     oid = id(edge_index)
     ref = weakref.ref(edge_index, lambda _r, oid=oid: _BY_ID.pop(oid, None))
     with _LOCK:

@@ -127,7 +127,7 @@ class TemporalGNN(_GATStack):
         if self._fused():
             from . import fused
             return fused.gru_head(self.gru, self.out, h, hidden_state)
-        if h.is_cuda and self.gru.bias and self.out.in_features == self.hidden_channels == 64:
+        if h.is_cuda and self._device_head_ok():
             # training / autograd: GRUCell + Linear forward and backward on the
             # device (gfd.fused.tgn_head_train); h0 = None is the reference's zeros
             from . import fused
@@ -136,6 +136,15 @@ class TemporalGNN(_GATStack):
             hidden_state = x.new_zeros((x.size(0), self.hidden_channels))
         new_hidden = self.gru(h, hidden_state)
         return _head(self.out, new_hidden), new_hidden
+
+    def _device_head_ok(self) -> bool:
+        """The head kernels' set: GRUCell(64, 64) with biases, Linear(64, <= 64),
+        fp32 parameters (anything else -- e.g. a .double() model -- takes the
+        torch GRUCell + Linear path instead of being read as fp32)."""
+        g, o = self.gru, self.out
+        params = list(g.parameters()) + list(o.parameters())
+        return (g.bias and g.input_size == g.hidden_size == 64 and o.in_features == 64 and
+                o.out_features <= 64 and all(p.dtype == torch.float32 for p in params))
 
     def predict(self, x, edge_index, batch=None, hidden_state=None,
                 apply_sigmoid: bool = True) -> torch.Tensor:

@@ -87,14 +87,18 @@ class NeighborSampler:
                                self.graph.device)
         return mn.value, me.value, self._ws[ns]
 
-    def sample(self, seeds: torch.Tensor, seed: Optional[int] = None) -> SampledBatch:
+    def sample(self, seeds: torch.Tensor, seed: Optional[int] = None,
+               _unique: bool = False) -> SampledBatch:
+        """``_unique``: the caller guarantees distinct seeds (NeighborLoader's
+        batches are slices of a permutation of input nodes it checked once), so
+        the per-batch sort + host sync of the duplicate check is skipped."""
         g = self.graph
         dev = g.device
         seeds = seeds.to(device=dev, dtype=torch.int64).contiguous()
         ns = seeds.numel()
         if ns == 0:
             raise ValueError("empty seed batch")
-        if torch.unique(seeds).numel() != ns:
+        if not _unique and torch.unique(seeds).numel() != ns:
             # the relabelling keeps one local id per node: a repeated seed
             # would silently lose its copy
             raise ValueError("seed batch holds duplicate node ids")
@@ -156,7 +160,8 @@ class NeighborLoader:
             idx = idx[torch.randperm(idx.numel(), generator=gen, device=idx.device)]
         for b in range(len(self)):
             seeds = idx[b * self.batch_size:(b + 1) * self.batch_size]
-            batch = self.sampler.sample(seeds, seed=batch_seed(self.seed, self.epoch, b))
+            batch = self.sampler.sample(seeds, seed=batch_seed(self.seed, self.epoch, b),
+                                        _unique=True)
             batch.x = self.x[batch.n_id]
             if self.y is not None:
                 batch.y = self.y[batch.n_id]
