@@ -230,6 +230,7 @@ namespace gfd {
 namespace fwd {
 
 gfd_status launch_fused(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
+  if (a.ep.hout) return GFD_ERR_UNSUPPORTED;  // the model head is folded by the tile kernels
   if (a.num_dst <= 0) return GFD_OK;
   if ((a.num_dst + kTile - 1) / kTile > 0x7fffffff) return GFD_ERR_UNSUPPORTED;
   return a.xdt == GFD_DTYPE_BF16 ? launch_fused_x<XBF16>(a, L, stream)

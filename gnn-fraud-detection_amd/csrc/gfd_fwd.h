@@ -466,7 +466,22 @@ struct Epi {
   const float* res;
   int64_t ldr;
   int64_t ldo = C;  // output row stride (floats): out row i at out + i * ldo
+  // the model head Linear(C, 1) (gat.py:94) folded into the store: hout[i] =
+  // y_i . hw + hb[0] is written INSTEAD of the row (hout == NULL: no head)
+  const float* hw = nullptr;
+  const float* hb = nullptr;
+  float* hout = nullptr;
 };
+
+// Sum over the 16 lanes of a DPP row (lanes 16 k .. 16 k + 15): every lane
+// of the row ends with the row's sum (the head's dot over 16 columns).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
+  return v;
+}
 
 __device__ __forceinline__ float epi_store_value(float v, float bias_n, int n, int64_t row,
                                                  const Epi& e) {

@@ -181,6 +181,7 @@ gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t N, int F,
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   const gfd_plan p = plan_or_empty(plan);
+  if (!out && ep && ep->head_out) out = ep->head_out;  // rows not written: the head replaces them
   gfd_status s =
       check_agg_args(x, x_dtype, N, F, ldx, rowptr, col, num_dst, dst_offset, dp, p, out);
   if (s != GFD_OK) return s;
@@ -193,6 +194,10 @@ gfd_status gfd_gat_aggregate_split(const void* x, int x_dtype, int64_t N, int F,
     if (!ep->scale_shift || stats || dp > 0.f) return GFD_ERR_ARGUMENT;
     if (ep->residual && ep->residual_stride < channels) return GFD_ERR_ARGUMENT;
     e = Epi{ep->scale_shift, ep->relu ? 1 : 0, ep->residual, ep->residual_stride};
+    e.hw = ep->head_weight;
+    e.hb = ep->head_bias;
+    e.hout = ep->head_out;
+    if (e.hout && !e.hw) return GFD_ERR_ARGUMENT;
   }
   e.ldo = out_stride;
   if (num_dst == 0) return GFD_OK;
@@ -256,6 +261,7 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   const gfd_plan p = plan_or_empty(plan);
+  if (!out && ep && ep->head_out) out = ep->head_out;  // rows not written: the head replaces them
   gfd_status s = check_agg_args(x, x_dtype, N, F, ldx, rowptr, col, N, 0, dp, p, out);
   if (s != GFD_OK) return s;
   if (!weight || !att_src || !att_dst) return GFD_ERR_ARGUMENT;
@@ -264,6 +270,10 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
     if (!ep->scale_shift || stats || dp > 0.f) return GFD_ERR_ARGUMENT;
     if (ep->residual && ep->residual_stride < channels) return GFD_ERR_ARGUMENT;
     e = Epi{ep->scale_shift, ep->relu ? 1 : 0, ep->residual, ep->residual_stride};
+    e.hw = ep->head_weight;
+    e.hb = ep->head_bias;
+    e.hout = ep->head_out;
+    if (e.hout && !e.hw) return GFD_ERR_ARGUMENT;
   }
   if (ws_bytes < gfd_gat_fwd_workspace_size(N, N, F, heads, channels, p.num_hubs, p.num_chunks))
     return GFD_ERR_WORKSPACE;

@@ -194,12 +194,24 @@ k_logits_lone(
           __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers))) * wbu;
       // the row's t logits (columns 8..15) next to its s logits (0..7)
       const float tq = dpp_mov<0x128>(sv[q]);  // row_ror:8 within the 16-lane row
-      if (lq) {
+      if (lq) {  // uniform over the 16 lanes of the row (lane group g)
         const int64_t orow = t * 16 + src;
+        if (ep.hout) {  // model head: one dot per row instead of the row
+          float d = 0.f;
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-          out[orow * ep.ldo + ct * 16 + rl] =
-              epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl, orow, ep);
+          for (int ct = 0; ct < 4; ++ct)
+            d = fmaf(epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl,
+                                     orow, ep),
+                     ep.hw[ct * 16 + rl], d);
+          d = row16_sum(d);
+          if (rl == 0) ep.hout[orow] = d + (ep.hb ? ep.hb[0] : 0.f);
+        } else {
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct)
+            out[orow * ep.ldo + ct * 16 + rl] =
+                epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl,
+                                orow, ep);
+        }
         if (__builtin_expect(stats != nullptr, 0) && rl < H) {  // training (no dropout) only
           stats[orow * 16 + rl] = leaky(sv[q] + tq, slope);
           stats[orow * 16 + H + rl] = 1.0f;

@@ -118,11 +118,21 @@ __global__ void __launch_bounds__(kLWaves * 64) k_lone(
       const int src = 4 * g + q;
       const int orow = __builtin_amdgcn_ds_bpermute(src << 2, row);
       const float ou = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(uns)));
-      if (orow >= 0) {
+      if (orow >= 0) {  // uniform over the 16 lanes of the row (lane group g)
+        if (ep.hout) {    // model head: one dot per row instead of the row
+          float d = 0.f;
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-          out[int64_t(orow) * ep.ldo + ct * 16 + r] =
-              epi_store_value(acc[ct][q] * ou, bc[ct], ct * 16 + r, orow, ep);
+          for (int ct = 0; ct < 4; ++ct)
+            d = fmaf(epi_store_value(acc[ct][q] * ou, bc[ct], ct * 16 + r, orow, ep),
+                     ep.hw[ct * 16 + r], d);
+          d = row16_sum(d);
+          if (r == 0) ep.hout[orow] = d + (ep.hb ? ep.hb[0] : 0.f);
+        } else {
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct)
+            out[int64_t(orow) * ep.ldo + ct * 16 + r] =
+                epi_store_value(acc[ct][q] * ou, bc[ct], ct * 16 + r, orow, ep);
+        }
       }
     }
     if (__builtin_expect(stats != nullptr, 0) && row >= 0) {  // training (no dropout) only

@@ -362,6 +362,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   float* rsc0 = reinterpret_cast<float*>(ring0 + 2 * kTile);    // [2][16] by tile parity
   int* rid0 = reinterpret_cast<int*>(rsc0 + 2 * kTile);         // [2][16]
   uint4* WL = reinterpret_cast<uint4*>(rid0 + 2 * kTile);       // [8 waves][LO][64]
+  // model head (ep.hout): per-tile row-dot partials of the 4 column tiles and
+  // the rows, by tile parity (written by the kh = 0 waves in reduce_store,
+  // summed by wave 4 after the next barrier 1)
+  float* hpart = reinterpret_cast<float*>(WL + kSWaves * LO * 64);  // [2][4 ct][16]
+  int* hrow = reinterpret_cast<int*>(hpart + 2 * 4 * kTile);         // [2][16]
 
   const int wave = wave_uniform(threadIdx.x >> 6);
   const int ct = wave & 3, kh = wave >> 2;
@@ -453,11 +458,38 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const int* rid = rid0 + tpar * kTile;
     const f32x4 sum = acc + red0[(tpar * 4 + ct) * 64 + lane];
     const int n = ct * 16 + (lane & 15);
+    if (ep.hout) {  // kernel-uniform: the head's dot over this wave's 16 columns
+      const float w = ep.hw[n];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = (lane >> 4) * 4 + q;
+        const int ri = rid[r];
+        const float v = ri >= 0 ? epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep) * w
+                                : 0.f;
+        const float d = row16_sum(v);  // lanes 16 k .. 16 k + 15 hold row 4 k + q
+        if ((lane & 15) == 0) {
+          hpart[(tpar * 4 + ct) * kTile + r] = d;
+          if (ct == 0) hrow[tpar * kTile + r] = ri;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = (lane >> 4) * 4 + q;
       const int ri = rid[r];
       if (ri >= 0) out[int64_t(ri) * ep.ldo + n] = epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep);
+    }
+  };
+  // the head's outputs of a finished tile: the four column tiles' partials in
+  // a fixed order (wave 4, after the barrier that follows reduce_store)
+  auto head_out = [&](int tpar) {
+    if (wave == 4 && lane < kTile) {
+      const int ri = hrow[tpar * kTile + lane];
+      const float* hp = hpart + tpar * 4 * kTile + lane;
+      if (ri >= 0)
+        ep.hout[ri] = ((hp[0] + hp[kTile]) + (hp[2 * kTile] + hp[3 * kTile])) +
+                      (ep.hb ? ep.hb[0] : 0.f);
     }
   };
   f32x4 acc_prev = {0.f, 0.f, 0.f, 0.f};  // kh = 0: tile v - 1, stored during MFMA(v)
@@ -551,6 +583,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #endif
 
     // ---- tile v + 1: aggregate its rows into Z ----
+    if (ep.hout && v > 0) head_out(pn);  // tile v - 1 (its partials: before barrier 1)
     if (more) aggregate(pn);
 #ifdef GFD_PROF
     const unsigned long long ts3 = __builtin_amdgcn_s_memtime();
@@ -574,12 +607,17 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #endif
 #undef GFD_ISSUE
   if (!kh) reduce_store(acc_prev, int((nv - 1) & 1));  // last tile
+  if (ep.hout) {  // kernel-uniform
+    __syncthreads();
+    head_out(int((nv - 1) & 1));
+  }
 }
 
 size_t stream_smem(int Fp, int lo) {
   return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 2 * 4 * 64 +
          sizeof(SlotRing) * 2 * kTile + sizeof(float) * 4 * kTile +
-         sizeof(uint4) * kSWaves * lo * 64;
+         sizeof(uint4) * kSWaves * lo * 64 + sizeof(float) * 2 * 4 * kTile +
+         sizeof(int) * 2 * kTile;
 }
 
 template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>

@@ -24,7 +24,8 @@ P = ct.c_void_p
 class GfdEpilogue(ct.Structure):
     """``gfd_epilogue`` (include/gfd.h)."""
     _fields_ = [("scale_shift", P), ("relu", ct.c_int), ("residual", P),
-                ("residual_stride", c_i64)]
+                ("residual_stride", c_i64), ("head_weight", P), ("head_bias", P),
+                ("head_out", P)]
 
 
 class GfdPlan(ct.Structure):

@@ -51,9 +51,20 @@ def bn_affine(bn: Optional[torch.nn.BatchNorm1d], device) -> torch.Tensor:
     return torch.cat([scale, shift]).contiguous()
 
 
+def head_foldable(head, width: int) -> bool:
+    """The model head the store can fold (gfd_epilogue.head_*): Linear(64, 1)
+    in fp32 after a layer whose input width takes the plan-scheduled kernels."""
+    return (head is not None and head.in_features == C and head.out_features == 1 and
+            head.weight.dtype == torch.float32 and head.weight.is_cuda and width <= 168 and
+            (head.bias is None or head.bias.dtype == torch.float32))
+
+
 def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
-              residual: bool = False) -> torch.Tensor:
-    """One eval-mode layer body: residual(h) + relu(bn(conv(h, edge_index)))."""
+              residual: bool = False, head=None) -> torch.Tensor:
+    """One eval-mode layer body: residual(h) + relu(bn(conv(h, edge_index))).
+    ``head`` (Linear(64, 1), see head_foldable): the model head folded into
+    the store (gat.py:94) -- returns head(body) [N, 1] and the [N, 64] body
+    is never written."""
     if torch.is_grad_enabled() and (h.requires_grad or conv.lin_src.weight.requires_grad):
         raise RuntimeError("gfd.fused.gat_layer is inference-only (use torch.no_grad())")
     dev = h.device
@@ -71,18 +82,26 @@ def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
             raise ValueError("residual needs the layer input width to equal 64")
         # the epilogue adds fp32 rows (gfd_epilogue.residual is float*)
         res = x if x.dtype == torch.float32 else x.float()
+    hout = hw = None
+    if head is not None:
+        if not head_foldable(head, F):
+            raise ValueError("gat_layer head: Linear(64, 1) fp32 on the device (head_foldable)")
+        hw = head.weight.detach().reshape(-1).contiguous()
+        hout = torch.empty((N, 1), dtype=torch.float32, device=dev)
     ep = _lib.GfdEpilogue(ab.data_ptr(), 1 if relu else 0, _lib.ptr(res),
-                          res.stride(0) if res is not None else 0)
+                          res.stride(0) if res is not None else 0, _lib.ptr(hw),
+                          _lib.ptr(head.bias.detach() if head is not None and
+                                   head.bias is not None else None), _lib.ptr(hout))
     plan = graph.plan()
     lib = _lib.load()
-    out = torch.empty((N, C), dtype=torch.float32, device=dev)
+    out = torch.empty((N, C), dtype=torch.float32, device=dev) if hout is None else None
     ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, plan.num_hubs, plan.num_chunks), dev)
     _lib.call("gfd_gat_fwd_ep", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
               graph.rowptr.data_ptr(), graph.col.data_ptr(), W.data_ptr(), a_s.data_ptr(),
               a_d.data_ptr(), _lib.ptr(bias), H, C, float(conv.negative_slope), 0.0, 0,
-              plan.cstruct(), _lib.ct.byref(ep), out.data_ptr(), None, None, ws.data_ptr(),
+              plan.cstruct(), _lib.ct.byref(ep), _lib.ptr(out), None, None, ws.data_ptr(),
               ws.numel(), _lib.stream_handle(dev))
-    return out
+    return out if hout is None else hout
 
 
 def gru_head(gru: torch.nn.GRUCell, lin: torch.nn.Linear, h: torch.Tensor,

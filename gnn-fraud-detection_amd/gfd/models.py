@@ -55,14 +55,18 @@ class _GATStack(nn.Module):
         GATConv launch chain with BN/ReLU/residual in the store epilogue."""
         return not self.training and not torch.is_grad_enabled()
 
-    def encode(self, x: torch.Tensor, edge_index) -> torch.Tensor:
+    def encode(self, x: torch.Tensor, edge_index, head=None) -> torch.Tensor:
+        """The layer stack; in inference, ``head`` (fused.head_foldable) is
+        folded into the last layer's store and its [N, 1] output returned."""
         h = x
         if self._fused():
             from . import fused
+            last = len(self.gat_layers) - 1
             for layer, conv in enumerate(self.gat_layers):
                 bn = self.batch_norms[layer] if self.batch_norms is not None else None
                 h = fused.gat_layer(conv, bn, h, edge_index, relu=True,
-                                    residual=self.residual and h.size(-1) == self.hidden_channels)
+                                    residual=self.residual and h.size(-1) == self.hidden_channels,
+                                    head=head if layer == last else None)
             return h
         for layer, conv in enumerate(self.gat_layers):
             y = conv(h, edge_index)
@@ -103,6 +107,13 @@ class GAT(_GATStack):
         self.out = nn.Linear(hidden_channels, out_channels)
 
     def forward(self, x, edge_index, batch: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if self._fused() and x.is_cuda and self.gat_layers:
+            from .fused import head_foldable
+            width = self.gat_layers[-1].in_channels
+            if head_foldable(self.out, width):
+                # inference: Linear(64, 1) folded into the last layer's store
+                # (gat.py:94): the [N, 64] body is never written or re-read
+                return self.encode(x, edge_index, head=self.out)
         return _head(self.out, self.encode(x, edge_index))
 
     def predict(self, x, edge_index, batch=None, apply_sigmoid: bool = True) -> torch.Tensor:

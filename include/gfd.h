@@ -340,6 +340,13 @@ typedef struct gfd_epilogue {
   int relu;
   const float* residual;    /* device [N, residual_stride] or NULL */
   int64_t residual_stride;
+  /* ABI 4: the model head Linear(C, 1) (gat.py:94) folded into the store of
+   * the last layer: head_out[i] = y_i . head_weight + head_bias[0] is written
+   * INSTEAD of the output row y_i (out may then be NULL).  head_out NULL: no
+   * head.  Plan-scheduled path only (F <= 168); GFD_ERR_UNSUPPORTED else. */
+  const float* head_weight; /* device [C] */
+  const float* head_bias;   /* device [1] or NULL */
+  float* head_out;          /* device [rows] */
 } gfd_epilogue;
 
 /* gfd_gat_fwd followed by the epilogue (ep may be NULL = gfd_gat_fwd).  With

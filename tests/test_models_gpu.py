@@ -264,3 +264,31 @@ def test_state_dict_roundtrip_keeps_lin_alias(golden):
         assert sd[f"gat_layers.{i}.lin_src.weight"].data_ptr() == \
             sd[f"gat_layers.{i}.lin_dst.weight"].data_ptr()
     assert m.gat_layers[0].lin_dst is m.gat_layers[0].lin_src
+
+
+@pytest.mark.parametrize("layers,F", [(3, 165), (1, 166)])
+def test_gat_head_folded_into_last_layer_store(layers, F):
+    """Inference: the GAT head Linear(64, 1) (gat.py:94) folded into the last
+    layer's store (gfd_epilogue.head_*: a row dot in the tile / lone / logits
+    kernels instead of writing [N, 64] and re-reading it) against the body
+    written out and the head applied by ATen, on a graph with hubs, general,
+    light and self-loop-only rows."""
+    from gfd import synth
+    from gfd.models import GAT
+    torch.manual_seed(11)
+    N = 20000
+    ei = torch.from_numpy(synth.power_law(N, 160000, seed=11)).to(DEV)
+    x = torch.randn(N, F, device=DEV)
+    m = GAT(F, 64, 1, num_layers=layers).to(DEV).eval()
+    with torch.no_grad():
+        for bn in m.batch_norms:
+            bn.running_mean.normal_()
+            bn.running_var.uniform_(0.5, 2.0)
+        for conv in m.gat_layers:
+            conv.bias.normal_()
+        m.out.bias.normal_()
+        folded = m(x, ei)
+        body = m.encode(x, ei)
+        want = body @ m.out.weight.t() + m.out.bias
+    assert folded.shape == (N, 1)
+    assert_close(folded, want, what=f"folded head, {layers} layers")
