@@ -2,7 +2,7 @@
 the tile stage's assumptions.
 
 * C4 exactly as bench.py builds and runs it (bench.setup + bench.Layer: 10M
-  nodes / 50M edges, F = 166 at row pitch 168 -- x is 6.7 GB, so rows above
+  nodes / 50M edges, F = 166 at row pitch 176 -- x is 7.0 GB, so rows above
   4 GiB are gathered -- the max|x| single-scale path, the class-scheduled
   tile stage): >= 512 sampled destinations (the 16 largest hubs, the 64
   highest node ids, 64 slots of each class, random) against the oracle, and
@@ -62,9 +62,11 @@ def c4():
 def test_c4_bench_configuration_sampled_parity(c4):
     import bench
     s = c4
-    assert s["ldx"] == 168 and s["x"].stride(0) == 168
+    # rows of 166 features + an 8-float source-logit slot at float 168 (pitch 176)
+    assert s["ldx"] == 176 and s["x"].stride(0) == 176 and s["s_row"] == (168, 176)
     assert s["xbuf"].numel() * 4 > 2 ** 32                 # x is past 4 GiB
     layer = bench.Layer(s, DEV, 1)
+    assert layer.in_row
     light_b, lone_b = layer.plan.classes()
     assert 0 < light_b < lone_b < s["graph"].num_nodes     # all three classes present
     assert layer.plan.num_hubs > 0
@@ -212,12 +214,14 @@ def test_bf16_features_match_fp32_oracle_on_rounded_x(F):
 
 
 def test_c5_shape_bf16_sampled_parity():
-    """The C5 generator and layout (bf16, row pitch 168) at 2M / 20M."""
+    """The C5 generator and layout (bf16 rows of 166 features + the 8-float
+    source-logit slot at byte 336: pitch 184) at 2M / 20M."""
     import bench
     s = bench.setup(DEV, 2_000_000, 20_000_000, 166, dtype=torch.bfloat16)
     s["bias"] = torch.randn(C, generator=torch.Generator().manual_seed(2)).to(DEV) * 0.1
-    assert s["ldx"] == 168 and s["x"].dtype == torch.bfloat16
+    assert s["ldx"] == 184 and s["x"].dtype == torch.bfloat16 and s["s_row"] == (84, 92)
     layer = bench.Layer(s, DEV, 1)
+    assert layer.in_row
     layer.step()
     torch.cuda.synchronize()
     dsts = _sample(layer, s)

@@ -2,7 +2,7 @@
 ("Next round" item 1).
 
 * C5 exactly as bench.py builds and times it (bench.setup: 50M nodes / 500M
-  input edges, bf16 x at row pitch 168, so element indices reach 8.4e9 > 2^32;
+  input edges, bf16 x at row pitch 184, so element indices reach 9.2e9 > 2^32;
   ~1.1M hub chunks, E' = 550M) through bench.Layer -- the fused logits + lone
   pass, hubs, general and light kernels -- compared with the oracle on >= 512
   sampled destinations: hubs spread over the hub ranks (the largest two
@@ -12,7 +12,7 @@
   which the logits over every row replace).
 * The backward (gat.py:80 under loss.backward(), train.py:142) on a C4-shaped
   graph at 2M nodes / 10M edges (hubs of thousands of messages, source hubs of
-  the CSC pass, x at pitch 168): grad_W, grad_att_src, grad_att_dst,
+  the CSC pass, x at pitch 176): grad_W, grad_att_src, grad_att_dst,
   grad_bias and grad_x against oracle.gatconv_grads_chunked (the PyG-dataflow
   autograd run in destination chunks, fp64, LeakyReLU kinks decided by the
   device's logits).
@@ -26,7 +26,7 @@ from _util import assert_close, assert_close_scaled
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 H, C = 8, 64
-ROW_PAST_2_32 = (2 ** 32) // 168 + 1     # first node whose bf16 row starts past element 2^32
+ROW_PAST_2_32 = (2 ** 32) // 184 + 1     # first node whose bf16 row starts past element 2^32
 
 
 def _reference(s, dsts, max_msgs=1_500_000):
@@ -84,7 +84,8 @@ def c5():
 def test_c5_full_size_sampled_parity(c5):
     import bench
     s = c5
-    assert s["ldx"] == 168 and s["x"].dtype == torch.bfloat16
+    # bf16 rows of 166 features + the 8-float source-logit slot (pitch 184)
+    assert s["ldx"] == 184 and s["x"].dtype == torch.bfloat16
     assert s["xbuf"].numel() > 2 ** 32                      # element indices past 2^32
     layer = bench.Layer(s, DEV, 1)
     light_b, lone_b = layer.plan.classes()
@@ -174,7 +175,7 @@ def test_backward_c4_shaped_2m_nodes():
     assert csc.plan.num_hubs > 0                            # source hubs (k_bwd_src chunks)
     gen = torch.Generator().manual_seed(6)
     bias = (torch.randn(C, generator=gen) * 0.1).to(DEV)
-    x = s["x"].detach().requires_grad_(True)                 # pitch-168 view
+    x = s["x"].detach().requires_grad_(True)                 # pitch-176 view
     W = s["W"].clone().requires_grad_(True)
     a_s = s["a_s"].clone().requires_grad_(True)
     a_d = s["a_d"].clone().requires_grad_(True)
