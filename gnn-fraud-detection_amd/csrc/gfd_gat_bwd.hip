@@ -635,9 +635,14 @@ __device__ __forceinline__ void src_segment(const int32_t* __restrict__ csc_dst,
 // into fp16 subnormals.
 // amax[m] (m < kDH): dh' column m; amax[kDH + f]: x column f, as float bits
 // (non-negative floats order like their bits: an integer max is exact and
-// order-independent).  kAmaxCols = kDH + 256 words.
+// order-independent).  The fused pass (k_src_gw) adds: amax[kGOff + c] max |g|
+// per channel, amax[kYHOff + c] max |y_hc| over the source-hub rows, and
+// amax[kTEOff] the largest non-hub out-degree (an integer).
 constexpr int kXCols = 256;  // x columns (F <= 256)
-constexpr int kAmaxCols = kDH + kXCols;
+constexpr int kGOff = kDH + kXCols;
+constexpr int kYHOff = kGOff + C;
+constexpr int kTEOff = kYHOff + C;
+constexpr int kAmaxCols = kTEOff + 16;
 
 __device__ __forceinline__ void amax_put(uint32_t* __restrict__ amax, int c, float v) {
   const uint32_t bits = __float_as_uint(v);
@@ -793,7 +798,7 @@ __global__ void __launch_bounds__(512) k_bwd_src_hub2(
     const float* __restrict__ spart, const int32_t* __restrict__ chunk_ptr,
     const int32_t* __restrict__ hub_src, const float* __restrict__ dt,
     const float* __restrict__ att_src, const float* __restrict__ att_dst,
-    float* __restrict__ dh, uint32_t* __restrict__ amax, int32_t* __restrict__ erow) {
+    float* __restrict__ dh, uint32_t* __restrict__ amax, int32_t* __restrict__ erow, int compact) {
   const int lane = threadIdx.x & 63, hh = threadIdx.x >> 6;
   const int64_t hb = blockIdx.x;
   const int c0 = chunk_ptr[hb], c1 = chunk_ptr[hb + 1];
@@ -804,10 +809,20 @@ __global__ void __launch_bounds__(512) k_bwd_src_hub2(
     if (hh == 0 && lane < 8) ds += r[HC + lane];
   }
   const int64_t j = hub_src[hb];
-  float* r = dh + j * kDH;
   __shared__ float sds[8];  // wave 0's ds, for every head's wave
   if (hh == 0 && lane < 8) sds[lane] = ds;
   __syncthreads();
+  if (compact) {  // the fused pass's hub rows: [y (raw) | ds | dt], row hb
+    float* r = dh + hb * kDH;
+    r[hh * C + lane] = y;
+    amax_put(amax, kYHOff + lane, fabsf(y));
+    if (hh == 0 && lane < 8) {
+      r[HC + lane] = sds[lane];
+      r[HC + H + lane] = dt[j * 8 + lane];
+    }
+    return;
+  }
+  float* r = dh + j * kDH;
   const float dth = dt[j * 8 + hh];
   const float v = fmaf(dth, att_dst[hh * C + lane],
                        fmaf(sds[hh], att_src[hh * C + lane], y * (1.0f / H)));
@@ -1029,6 +1044,560 @@ __global__ void __launch_bounds__(512) k_gw(const float* __restrict__ dh,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused source pass + grad_W' GEMM (grad_x not requested: the first layer,
+// F = 166 at C4).  The source side's rows are formed in LDS, a K tile of 32
+// source nodes at a time, and go straight into the f16 MFMA: no 2,112-B dh'
+// row makes the HBM round trip (21 GB each way at C4).  The GEMM runs on the
+// unfolded rows [y (512) | ds (8) | dt (8)]; the fold
+//   grad_W_h = (Y_h^T x) / H + a_src,h (x) S_h + a_dst,h (x) T_h
+// (S, T = the ds / dt rows of the product) is applied to the reduced 528 x F
+// result by k_fold_gw -- exactly the dh' = y/H + ds a_src + dt a_dst of the
+// unfused path, by linearity.
+//  * scales: a y column (head h, channel c) is bounded by keep x (largest
+//    non-hub out-degree) x max_i |g_ic| (and by the source-hub rows' own
+//    maxima), one power of two per channel for the launch, so the y tiles
+//    accumulate in the MFMA; the 8 ds / dt rows take the tile's exact maxima
+//    and their product is added times its inverse scales.
+//  * block = (slab s of source nodes, half): half 0 = y heads 0-3 and ds,
+//    half 1 = y heads 4-7 and dt.  The two halves of a slab run on one XCD
+//    back to back, so their g-row gathers and x tiles meet in its L2.  Slabs
+//    are balanced by non-hub messages + a fixed cost per tile (k_slab_bounds).
+//  * y phase: the tile's messages (CSC order; source hubs excluded -- their
+//    rows come compact from k_bwd_src_hub2) are split evenly over the 8
+//    waves.  A wave walks its range in chunks of 32 (4 batches of 8: lane = 8
+//    slot + head for the indices and records, lane = channel for the g rows)
+//    and accumulates y (this half's 4 heads) and ds (8 heads) per source; a
+//    source's sum goes to its LDS row, or, for a source begun by an earlier
+//    wave, to this wave's head-partial row (merged in wave order after the
+//    barrier).  The next tile's first chunk indices are loaded during this
+//    tile's column pass, its records and g rows during the MFMAs' tail.
+//  * column pass: thread (column m, node half) scales and splits the 16 values
+//    into f16 hi / lo (the k_gw image: [row][node]).
+//  * MFMA as k_gw: wave (wm, wn) holds y m-tiles wm + 4 i, n-tiles wn + 2 j;
+//    the ds / dt m-tile (16) is spread over the waves by n-tile.
+constexpr int kFK = 32;         // source nodes per K tile
+constexpr int kFR = 272;        // A rows per half: y 256 | ds or dt 8 | zero 8
+constexpr int kFE = 264;        // A rows that carry values
+constexpr int kFYP = 266;       // y-tile pitch in floats: y 256 | ds 8 (2 mod 4: the column
+                                // pass's two node halves sit on opposite LDS banks)
+constexpr int kFNB = 4;         // batches of 8 messages per chunk
+constexpr int kFCh = 8 * kFNB;  // messages per chunk
+constexpr int kFCost = 128;     // slab balance: a tile's fixed cost, in messages
+constexpr int kFMaxFu = 192;    // the fused path's feature bound (NJ = 6)
+
+struct FLay {
+  int yt, hp, ahi, alo, bhi, blo, ysc, yinv, iax, csb, dtt, pw, cw, hrk, hpr, bytes;
+};
+
+__host__ __device__ inline FLay flay(int Fu) {
+  FLay L;
+  int o = 0;
+  auto take = [&o](int bytes) {
+    const int r = o;
+    o += (bytes + 15) / 16 * 16;
+    return r;
+  };
+  L.yt = take(kFK * kFYP * 4);
+  L.hp = take(8 * kFYP * 4);
+  L.ahi = take(kFR * kGPt * 2);
+  L.alo = take(kFR * kGPt * 2);
+  L.bhi = take(Fu * kGPt * 2);
+  L.blo = take(Fu * kGPt * 2);
+  L.ysc = take(C * 4);
+  L.yinv = take(C * 4);
+  L.iax = take(16 * 4);
+  L.csb = take(kGMaxF * 4);
+  L.dtt = take(kFK * 8 * 4);
+  L.pw = take(8 * 33 * 4);
+  L.cw = take(8 * 32 * 4);
+  L.hrk = take(kFK * 4);
+  L.hpr = take(8 * 4);
+  L.bytes = o;
+  return L;
+}
+
+template <typename XT, bool VEC, int NJ>
+__global__ void __launch_bounds__(512) k_src_gw(
+    const int32_t* __restrict__ colptr, const int32_t* __restrict__ csc_dst,
+    const int32_t* __restrict__ csc_eid, const int32_t* __restrict__ src_hub_rank,
+    const float* __restrict__ dhub, const float* __restrict__ rec, const float* __restrict__ dt,
+    const float* __restrict__ g, float keep, const typename XT::T* __restrict__ x, int64_t ldx,
+    int F, int Fu, const int32_t* __restrict__ bounds, int S, const uint32_t* __restrict__ amax,
+    float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) char fsm[];
+  const FLay L = flay(Fu);
+  float* yt = reinterpret_cast<float*>(fsm + L.yt);
+  float* hp = reinterpret_cast<float*>(fsm + L.hp);
+  _Float16* Ahi = reinterpret_cast<_Float16*>(fsm + L.ahi);
+  _Float16* Alo = reinterpret_cast<_Float16*>(fsm + L.alo);
+  _Float16* Bhi = reinterpret_cast<_Float16*>(fsm + L.bhi);
+  _Float16* Blo = reinterpret_cast<_Float16*>(fsm + L.blo);
+  float* ysc = reinterpret_cast<float*>(fsm + L.ysc);
+  float* yinv = reinterpret_cast<float*>(fsm + L.yinv);
+  float* iax = reinterpret_cast<float*>(fsm + L.iax);
+  float* csb = reinterpret_cast<float*>(fsm + L.csb);
+  float* dtt = reinterpret_cast<float*>(fsm + L.dtt);
+  int* pw = reinterpret_cast<int*>(fsm + L.pw);
+  int* cw = reinterpret_cast<int*>(fsm + L.cw);
+  int* hrk = reinterpret_cast<int*>(fsm + L.hrk);
+  int* hpr = reinterpret_cast<int*>(fsm + L.hpr);
+
+  const int b = blockIdx.x, rem = b & 15;
+  const int half = rem >> 3, s = (b >> 4) * 8 + (rem & 7);
+  if (s >= S) return;  // block-uniform, before any barrier
+  const int64_t kb = bounds[s], ke = bounds[s + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar ranges
+  const int wm = wave & 3, wn = wave >> 2;
+  const int NTn = Fu >> 4, nB = 16 * (Fu >> 2);
+
+  if (tid < C) {
+    const float te = float(amax[kTEOff]);
+    float bound = keep * te * __uint_as_float(amax[kGOff + tid]);
+    bound = fmaxf(fminf(bound, 3.0e38f), __uint_as_float(amax[kYHOff + tid]));
+    const int e = scale_exp(bound);
+    ysc[tid] = ldexpf(1.0f, e);
+    yinv[tid] = ldexpf(1.0f, -e);
+  }
+  if (tid < kGMaxF)
+    csb[tid] = tid < F ? ldexpf(1.0f, scale_exp(__uint_as_float(amax[kDH + tid]))) : 1.0f;
+  for (int i = tid; i < (kFR - kFE) * kGPt; i += 512) {
+    Ahi[kFE * kGPt + i] = _Float16(0.f);
+    Alo[kFE * kGPt + i] = _Float16(0.f);
+  }
+  if (tid >= 8 && tid < 16) iax[tid] = 0.f;
+  for (int i = tid; i < (kFK + 8) * kFYP; i += 512) yt[i] = 0.f;  // yt, hp adjacent
+  __syncthreads();
+
+  int* P = pw + wave * 33;  // this wave's copy of the tile's message prefix
+  int* Cs = cw + wave * 32;  // and of its sources' CSC starts
+  // largest r in [0, 32) with P[r] <= f (P non-decreasing; f < P[32])
+  auto find = [&](int f) {
+    int r = 0;
+#pragma unroll
+    for (int st = 16; st >= 1; st >>= 1)
+      if (P[r + st] <= f) r += st;
+    return r;
+  };
+
+  // --- per-wave pipeline state ---
+  int n_c0 = 0, n_c1 = 0, n_hr = -1;  // next tile: lane r's source colptr pair, hub rank
+  float n_dt = 0.f;                   // next tile: dt of node 4 wave + (lane >> 3), head lane & 7
+  int code = -2;                      // tile's lane r: hub rank | -1 | -2 outside | -3 no messages
+  int lo = 0, hi = 0, rfirst = 0;     // the wave's message range in the tile, its first source
+  bool head = false;                  // ... begun by an earlier wave
+  int pe[kFNB], pi[kFNB], rr[kFNB];   // chunk: edge ids, destinations, source per slot
+  float pa[kFNB], pd[kFNB], pg[kFNB][8];  // chunk: alpha~, dpre (lane 8 slot + head), g rows
+
+  auto load_next = [&](int64_t k0) {
+    const int64_t j = k0 + (lane & 31);
+    const int64_t jc = (lane < 32 && j < ke) ? j : kb;
+    n_c0 = colptr[jc];
+    n_c1 = colptr[jc + 1];
+    if (src_hub_rank) n_hr = src_hub_rank[jc];
+    const int64_t jd = k0 + 4 * wave + ((lane >> 3) & 3);
+    n_dt = dt[(jd < ke ? jd : kb) * 8 + (lane & 7)];
+  };
+  auto issue_idx = [&](int c) {
+#pragma unroll
+    for (int bb = 0; bb < kFNB; ++bb) {
+      const int f = c + 8 * bb + (lane >> 3);
+      const bool ok = f < hi;
+      const int r = find(ok ? f : c);
+      const int p = ok ? Cs[r] + (f - P[r]) : 0;
+      pe[bb] = csc_eid[p];
+      pi[bb] = csc_dst[p];
+      rr[bb] = ok ? r : -1;
+    }
+  };
+  auto issue_data = [&]() {
+#pragma unroll
+    for (int bb = 0; bb < kFNB; ++bb) {
+      const float* rp = rec + int64_t(pe[bb]) * kRec + (lane & 7);
+      pa[bb] = rp[0];
+      pd[bb] = rp[H];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {  // a uniform row base: the saddr + lane-offset form
+        const float* gr = g + int64_t(__builtin_amdgcn_readlane(pi[bb], 8 * kk)) * C;
+        pg[bb][kk] = gr[lane];
+      }
+    }
+  };
+  // the tile's prefix, the wave's range, and its first chunk's indices
+  auto prep = [&](int64_t k0) {
+    const int64_t j = k0 + (lane & 31);
+    const bool in = lane < 32 && j < ke;
+    const int hr = in ? n_hr : -2;
+    const int d = (in && hr < 0) ? n_c1 - n_c0 : 0;
+    code = hr >= 0 ? hr : (hr == -2 ? -2 : (d > 0 ? -1 : -3));
+    int inc = d;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+      const int t = __shfl_up(inc, off);
+      if (lane >= off) inc += t;
+    }
+    const int D = __builtin_amdgcn_readlane(inc, 31);
+    if (lane < 32) {
+      P[lane] = inc - d;
+      Cs[lane] = n_c0;
+    }
+    if (lane == 0) P[32] = D;
+    lo = int((int64_t(wave) * D) >> 3);
+    hi = int((int64_t(wave + 1) * D) >> 3);
+    if (lo < hi) {
+      rfirst = __builtin_amdgcn_readfirstlane(find(lo));
+      head = lo > P[rfirst];
+      issue_idx(lo);
+    } else {
+      head = false;
+    }
+  };
+
+  // accumulate a chunk's messages into the LDS rows: in program order, and no
+  // two waves ever add to the same row (owner rows vs head-partial rows), so the
+  // float sums have a fixed order.  Rows are zeroed by their readers.
+  float* hpw = hp + wave * kFYP;
+  auto add = [](float* p, float v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto consume = [&](int n) {
+    const int ln = opaque(lane);  // (LDS addresses recomputed, not pinned across the loop)
+#pragma unroll
+    for (int k = 0; k < kFCh; ++k) {
+      if (k < n) {
+        const int bb = k >> 3, kk = k & 7;
+        const int rk = __builtin_amdgcn_readlane(rr[bb], 8 * kk);
+        float* row = (head && rk == rfirst) ? hpw : yt + rk * kFYP;
+        const float gk = pg[bb][kk];
+#pragma unroll
+        for (int hl = 0; hl < 4; ++hl)
+          add(row + hl * 64 + ln,
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa[bb]), 8 * kk + 4 * half + hl)) *
+                  gk);
+        if (half == 0) {  // ds (heads: lanes 0..7); half 1 forms no ds row
+          const float dsk = __shfl(pd[bb], 8 * kk + (lane & 7));
+          if (ln < 8) add(row + 256 + ln, dsk);
+        }
+      }
+    }
+  };
+
+  // x tile: 2 items x 2 nodes x 4 columns per thread (k_gw's B staging)
+  f32x4 xs[2][2];
+  auto load_x = [&](int64_t k0, int tq) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int i = tq + 512 * it, p = i & 15, c = i >> 4;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int64_t r = k0 + 2 * p + e;
+        xs[it][e] = (r < ke && i < nB) ? gw_x4<XT, VEC>(x, ldx, F, r, 4 * c)
+                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto store_x = [&](int tq) {
+    uint32_t* bh = reinterpret_cast<uint32_t*>(Bhi);
+    uint32_t* bl = reinterpret_cast<uint32_t*>(Blo);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int i = tq + 512 * it, p = i & 15, c = i >> 4;
+      if (i < nB) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t l;
+          const float sb = csb[4 * c + q];
+          const uint32_t h = pk_hi_lo(xs[it][0][q] * sb, xs[it][1][q] * sb, l);
+          bh[((4 * c + q) * kGPt >> 1) + p] = h;
+          bl[((4 * c + q) * kGPt >> 1) + p] = l;
+        }
+      }
+    }
+  };
+  // 16 values of A row m (nodes 16 kh ..) scaled by sc -> f16 hi / lo image
+  auto put_row = [&](int m, int kh, const float (&v)[16], float sc) {
+    uint32_t hv[8], lv[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) hv[p] = pk_hi_lo(v[2 * p] * sc, v[2 * p + 1] * sc, lv[p]);
+    uint4* ah = reinterpret_cast<uint4*>(Ahi + m * kGPt + 16 * kh);
+    uint4* al = reinterpret_cast<uint4*>(Alo + m * kGPt + 16 * kh);
+    ah[0] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+    ah[1] = make_uint4(hv[4], hv[5], hv[6], hv[7]);
+    al[0] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+    al[1] = make_uint4(lv[4], lv[5], lv[6], lv[7]);
+  };
+  // y column m (< 256) over nodes 16 kh .. 16 kh + 15 (partials merged)
+  auto ycolumn = [&](int m, int kh) {
+    float v[16];
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const int k = 16 * kh + kk;
+      const float yv = yt[k * kFYP + m];
+      yt[k * kFYP + m] = 0.f;  // ready for the next tile's sums
+      v[kk] = hrk[k] == -1 ? yv : 0.f;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {  // source hubs: their compact rows (rare)
+      const int cd = hrk[16 * kh + kk];
+      if (cd >= 0) v[kk] = dhub[int64_t(cd) * kDH + 256 * half + m];
+    }
+    put_row(m, kh, v, ysc[m & 63]);
+  };
+  // ds (half 0) / dt (half 1) column e: the tile's exact max (lane pair)
+  auto xcolumn = [&](int e, int kh) {
+    float v[16];
+    float mx = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const int k = 16 * kh + kk;
+      const int cd = hrk[k];
+      float val;
+      if (half) {
+        val = cd == -2 ? 0.f : dtt[k * 8 + e];
+      } else {
+        val = cd == -1 ? yt[k * kFYP + 256 + e] : 0.f;
+        yt[k * kFYP + 256 + e] = 0.f;
+        if (cd >= 0) val = dhub[int64_t(cd) * kDH + HC + e];
+      }
+      v[kk] = val;
+      mx = fmaxf(mx, fabsf(val));
+    }
+    mx = fmaxf(mx, dpp_mov<0xB1>(mx));  // lane ^ 1: the column's other node half
+    const int ex = scale_exp(mx);
+    put_row(256 + e, kh, v, ldexpf(1.0f, ex));
+    if (kh == 0) iax[e] = ldexpf(1.0f, -ex);
+  };
+
+  f32x4 acc[4][NJ], accx[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  accx[0] = accx[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma_tile = [&]() {
+    const int ln = opaque(lane);
+    const int fo = (ln & 15) * kGPt + 8 * (ln >> 4);
+    f16x8 a_hi[4], a_lo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mt = wm + 4 * i;
+      a_hi[i] = *reinterpret_cast<const f16x8*>(Ahi + mt * 16 * kGPt + fo);
+      a_lo[i] = *reinterpret_cast<const f16x8*>(Alo + mt * 16 * kGPt + fo);
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nt = wn + 2 * j;
+      if (nt < NTn) {
+        const f16x8 b_hi = *reinterpret_cast<const f16x8*>(Bhi + nt * 16 * kGPt + fo);
+        const f16x8 b_lo = *reinterpret_cast<const f16x8*>(Blo + nt * 16 * kGPt + fo);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi[i], b_hi, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi[i], b_lo, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_lo[i], b_hi, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    const f16x8 x_hi = *reinterpret_cast<const f16x8*>(Ahi + 16 * 16 * kGPt + fo);
+    const f16x8 x_lo = *reinterpret_cast<const f16x8*>(Alo + 16 * 16 * kGPt + fo);
+    const f32x4 xsc = *reinterpret_cast<const f32x4*>(iax + 4 * (ln >> 4));
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2) {
+      const int nt = wave + 8 * j2;
+      if (nt < NTn) {
+        const f16x8 b_hi = *reinterpret_cast<const f16x8*>(Bhi + nt * 16 * kGPt + fo);
+        const f16x8 b_lo = *reinterpret_cast<const f16x8*>(Blo + nt * 16 * kGPt + fo);
+        f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(x_hi, b_hi, f32x4{0.f, 0.f, 0.f, 0.f},
+                                                         0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(x_hi, b_lo, t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(x_lo, b_hi, t, 0, 0, 0);
+        accx[j2] += t * xsc;
+      }
+    }
+  };
+
+  const int64_t T = (ke - kb + kFK - 1) / kFK;
+  if (T > 0) {
+    load_next(kb);
+    prep(kb);
+    if (lo < hi) issue_data();
+  }
+  for (int64_t t = 0; t < T; ++t) {
+    const int64_t k0 = kb + t * kFK;
+    // ---- y phase ----
+    if (wave == 0 && lane < 32) hrk[lane] = code;
+    if (lane < 32)
+      dtt[(4 * wave + (lane >> 3)) * 8 + (lane & 7)] =
+          k0 + 4 * wave + (lane >> 3) < ke ? n_dt : 0.f;
+    load_x(k0, opaque(tid));
+    if (t + 1 < T) load_next(k0 + kFK);
+    if (lo < hi) {
+      consume(min(hi - lo, kFCh));
+      for (int c = lo + kFCh; c < hi; c += kFCh) {  // long ranges: further chunks in place
+        issue_idx(c);
+        issue_data();
+        consume(min(hi - c, kFCh));
+      }
+    }
+    if (lane == 0) hpr[wave] = (lo < hi && head) ? rfirst : -1;
+    __syncthreads();
+    // ---- next tile's first chunk: prefix and indices ----
+    if (t + 1 < T) prep(k0 + kFK);
+    // ---- head partials into their owners' rows, in wave order (a fixed order) ----
+    {
+      bool any = false;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) any |= hpr[w] >= 0;
+      if (any) {  // block-uniform
+        const int tq = opaque(tid);
+        if (tq < kFE) {
+#pragma unroll 1
+          for (int w = 0; w < 8; ++w) {
+            const int r = hpr[w];
+            if (r >= 0) {
+              yt[r * kFYP + tq] += hp[w * kFYP + tq];
+              hp[w * kFYP + tq] = 0.f;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // ---- column pass ----
+    {
+      const int tq = opaque(tid);
+      store_x(tq);
+      ycolumn(tq >> 1, tq & 1);
+      if (tq < 16) xcolumn(tq >> 1, tq & 1);
+    }
+    __syncthreads();
+    if (t + 1 < T && lo < hi) issue_data();
+    // ---- MFMA ----
+    mfma_tile();
+  }
+
+  float* Cz = slab + int64_t(s) * kDH * F;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int mt = wm + 4 * i;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nt = wn + 2 * j;
+      const int n = nt * 16 + (lane & 15);
+      if (nt >= NTn || n >= F) continue;
+      const float ub = 1.0f / csb[n];  // exact: powers of two, undone in two steps
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ml = mt * 16 + 4 * (lane >> 4) + q;
+        Cz[int64_t(256 * half + ml) * F + n] = (acc[i][j][q] * yinv[ml & 63]) * ub;
+      }
+    }
+  }
+#pragma unroll
+  for (int j2 = 0; j2 < 2; ++j2) {
+    const int nt = wave + 8 * j2;
+    const int n = nt * 16 + (lane & 15);
+    if (nt >= NTn || n >= F) continue;
+    const float ub = 1.0f / csb[n];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ml = 4 * (lane >> 4) + q;
+      if (ml < kFE - 256) Cz[int64_t(HC + 8 * half + ml) * F + n] = accx[j2][q] * ub;
+    }
+  }
+}
+
+// grad_W = (Y^T x) / H + a_src (x) S + a_dst (x) T from the fused pass's
+// reduced [y 512 | S 8 | T 8] x F product (the unfused path's dh' fold)
+__global__ void __launch_bounds__(256) k_fold_gw(const float* __restrict__ gw,
+                                                 const float* __restrict__ att_src,
+                                                 const float* __restrict__ att_dst, int F,
+                                                 float* __restrict__ grad_W) {
+  const int64_t o = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (o >= int64_t(HC) * F) return;
+  const int hc = int(o / F), f = int(o - int64_t(hc) * F), h = hc / C;
+  grad_W[o] = fmaf(att_dst[hc], gw[int64_t(HC + H + h) * F + f],
+                   fmaf(att_src[hc], gw[int64_t(HC + h) * F + f], gw[o] * (1.0f / H)));
+}
+
+// Per 32-node tile of the fused pass: its non-hub messages + kFCost.
+__global__ void __launch_bounds__(256) k_tile_cost(const int32_t* __restrict__ colptr,
+                                                   const int32_t* __restrict__ hub_rank,
+                                                   int64_t N, int32_t* __restrict__ cost,
+                                                   uint32_t* __restrict__ amax) {
+  const int64_t nt = (N + kFK - 1) / kFK;
+  int dmax = 0;
+  for (int64_t u = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; u < nt;
+       u += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t j1 = min(N, (u + 1) * kFK);
+    int c = kFCost;
+    for (int64_t j = u * kFK; j < j1; ++j) {
+      if (!hub_rank || hub_rank[j] < 0) {
+        const int d = colptr[j + 1] - colptr[j];
+        c += d;
+        dmax = max(dmax, d);
+      }
+    }
+    cost[u] = c;
+  }
+  // the largest non-hub out-degree (the y-row scale bound)
+  for (int o = 32; o >= 1; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o));
+  if ((threadIdx.x & 63) == 0 && uint32_t(dmax) > __atomic_load_n(amax + kTEOff, __ATOMIC_RELAXED))
+    atomicMax(amax + kTEOff, uint32_t(dmax));
+}
+
+// One block: exclusive prefix of the tile costs (pre[nt] = total), then the
+// S + 1 slab bounds -- bounds[s] = 32 x the first tile whose prefix reaches
+// s / S of the total (bounds[0] = 0, bounds[S] = N).
+__global__ void __launch_bounds__(1024) k_slab_bounds(const int32_t* __restrict__ cost,
+                                                      int64_t nt, int S, int64_t N,
+                                                      int64_t* __restrict__ pre,
+                                                      int32_t* __restrict__ bounds) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (nt + 1023) / 1024;
+  const int64_t u0 = min(nt, int64_t(t) * per), u1 = min(nt, u0 + per);
+  int64_t sum = 0;
+  for (int64_t u = u0; u < u1; ++u) sum += cost[u];
+  part[t] = sum;
+  __syncthreads();
+  if (t == 0) {
+    int64_t run = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const int64_t v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    pre[nt] = run;
+  }
+  __syncthreads();
+  int64_t run = part[t];
+  for (int64_t u = u0; u < u1; ++u) {
+    pre[u] = run;
+    run += cost[u];
+  }
+  __syncthreads();
+  const int64_t total = pre[nt];
+  for (int sl = t; sl <= S; sl += 1024) {
+    int64_t bnd;
+    if (sl == 0) {
+      bnd = 0;
+    } else if (sl == S) {
+      bnd = N;
+    } else {
+      const int64_t target = total * sl / S;
+      int64_t a = 0, z = nt;  // smallest u with pre[u] >= target (pre[nt] = total)
+      while (a < z) {
+        const int64_t mid = (a + z) >> 1;
+        if (pre[mid] >= target) z = mid; else a = mid + 1;
+      }
+      bnd = min(N, a * kFK);
+    }
+    bounds[sl] = int32_t(bnd);
+  }
+}
+
 // grad_x = dh W for F <= 64 (hidden layers) on f16 MFMA 16x16x32 with the
 // 3-term split: A = dh rows (k = the 512 head-channel columns, contiguous in a
 // row: no transpose), scaled by 2^ea from max |dh'| (k_bwd_src); B = the
@@ -1201,10 +1770,18 @@ __global__ void __launch_bounds__(1024) k_reduce_few(const float* __restrict__ p
 // column sums of a [n, 64] fp32 matrix: fixed-grid partials part[block][64].
 // A wave reads 4 rows per 16-B-per-lane load (lane = row (lane >> 4), columns
 // 4 (lane & 15) ..), four such loads in flight per iteration, each into its
-// own accumulator; fixed summation order.
+// own accumulator; fixed summation order.  gmax (nullable): per-column max |a|
+// into gmax[0..63] (the fused pass's y-row scales).
 __global__ void __launch_bounds__(256) k_colsum64(const float* __restrict__ a, int64_t n,
-                                                  float* __restrict__ part) {
+                                                  float* __restrict__ part,
+                                                  uint32_t* __restrict__ gmax) {
   __shared__ float4 red[4][16];
+  __shared__ float4 redm[4][16];
+  float4 mx = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto fold_max = [&](const float4& v) {
+    mx.x = fmaxf(mx.x, fabsf(v.x)); mx.y = fmaxf(mx.y, fabsf(v.y));
+    mx.z = fmaxf(mx.z, fabsf(v.z)); mx.w = fmaxf(mx.w, fabsf(v.w));
+  };
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane & 15;
   const int64_t st = int64_t(gridDim.x) * 16;  // rows per sweep of the grid
   int64_t r = (int64_t(blockIdx.x) * 4 + w) * 4 + (lane >> 4);
@@ -1218,11 +1795,21 @@ __global__ void __launch_bounds__(256) k_colsum64(const float* __restrict__ a, i
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       s[k].x += v[k].x; s[k].y += v[k].y; s[k].z += v[k].z; s[k].w += v[k].w;
+      if (gmax) fold_max(v[k]);
     }
   }
   for (; r < n; r += st) {  // at most three rows left
     const float4 v = reinterpret_cast<const float4*>(a + r * C)[q];
     s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
+    if (gmax) fold_max(v);
+  }
+  if (gmax) {  // block-uniform
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      mx.x = fmaxf(mx.x, __shfl_xor(mx.x, m)); mx.y = fmaxf(mx.y, __shfl_xor(mx.y, m));
+      mx.z = fmaxf(mx.z, __shfl_xor(mx.z, m)); mx.w = fmaxf(mx.w, __shfl_xor(mx.w, m));
+    }
+    if (lane < 16) redm[w][q] = mx;
   }
   float4 t;
   t.x = (s[0].x + s[1].x) + (s[2].x + s[3].x);
@@ -1236,6 +1823,10 @@ __global__ void __launch_bounds__(256) k_colsum64(const float* __restrict__ a, i
   }
   if (lane < 16) red[w][q] = t;
   __syncthreads();
+  if (gmax && threadIdx.x < 64) {
+    const float* rm = reinterpret_cast<const float*>(redm);
+    amax_put(gmax, lane, fmaxf(fmaxf(rm[lane], rm[64 + lane]), fmaxf(rm[128 + lane], rm[192 + lane])));
+  }
   if (threadIdx.x < 64) {
     const float* rf = reinterpret_cast<const float*>(red);
     part[int64_t(blockIdx.x) * 64 + lane] =
@@ -1296,6 +1887,34 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
   L.gw = take(sizeof(float) * size_t(kDH) * F);
   L.gbp = take(sizeof(float) * size_t(kRedBlocks) * 64);
   return L;
+}
+
+// The fused source pass + grad_W' GEMM (k_src_gw) when grad_x is not
+// requested and F fits it; GFD_BWD_FUSED=0 selects the unfused dh' path (A/B).
+// Its scratch (tile costs, their prefix, the slab bounds) follows the compact
+// hub rows in the dh region, which the fused pass does not otherwise use.
+struct FusedPlan {
+  int S = 0;  // 0: unfused
+  int64_t nt = 0;
+  size_t scratch = 0, pre_off = 0, bounds_off = 0;
+};
+
+FusedPlan fused_plan(int64_t N, int F, int64_t shubs, bool want_gx) {
+  FusedPlan p;
+  const char* e = getenv("GFD_BWD_FUSED");
+  if (want_gx || (e && e[0] == '0') || (F + 15) / 16 * 16 > kFMaxFu) return p;
+  int64_t S = (N + 4095) / 4096;
+  if (S > cu_count()) S = cu_count();
+  if (S < 1) S = 1;
+  p.nt = (N + kFK - 1) / kFK;
+  p.scratch = align_up(sizeof(float) * size_t(shubs) * kDH, 256);
+  p.pre_off = align_up(sizeof(int32_t) * size_t(p.nt), 256);
+  p.bounds_off = p.pre_off + align_up(sizeof(int64_t) * size_t(p.nt + 1), 256);
+  const size_t need = p.scratch + p.bounds_off + sizeof(int32_t) * size_t(S + 1);
+  if (need > sizeof(float) * size_t(N) * kDH) return p;  // no room: unfused
+  if (size_t(flay((F + 15) / 16 * 16).bytes) > 160 * 1024) return p;
+  p.S = int(S);
+  return p;
 }
 
 template <typename XT, int KF>
@@ -1397,19 +2016,65 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   s = launch_msg_x<XT>(kf_fu(F), x, F, Fu, ldx, rowptr, col, N, plan, st, stats, g, whdr, bhi,
                        blo, slope, dp, seed, uhub, dpre, alpha_d, dt, cpart, hadot, stream);
   if (s != GFD_OK) return s;
-  // 3. source side: dh' rows
+  // 3. source side: dh' rows (and, fused, the grad_W' GEMM)
+  const bool xvec = ldx % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
   {
     int64_t blocks = (N + 3) / 4;
     if (blocks > 16384) blocks = 16384;
     GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
-    const bool xvec = ldx % 4 == 0 &&
-                      reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
     const unsigned xb = unsigned(blocks < 2048 ? blocks : 2048);
     if (xvec)
       k_xmax<XT, true><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
     else
       k_xmax<XT, false><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
     GFD_LAUNCH_CHECK();
+  }
+  const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr);
+  if (fp.S > 0) {
+    // source hubs first: their dh' rows, compact, at the start of the dh region
+    if (shubs > 0) {
+      k_bwd_src_hub1<<<unsigned((schunks + 3) / 4), 256, 0, stream>>>(
+          csc_dst, csc_eid, reinterpret_cast<const int4*>(src_plan->hub_chunk), schunks, alpha_d,
+          dpre, g, spart);
+      GFD_LAUNCH_CHECK();
+      k_bwd_src_hub2<<<unsigned(shubs), 512, 0, stream>>>(spart, src_plan->hub_chunk_ptr,
+                                                          src_plan->hub_dst, dt, att_src, att_dst,
+                                                          dh, amax, erow, 1);
+      GFD_LAUNCH_CHECK();
+    }
+    char* fz = reinterpret_cast<char*>(dh) + fp.scratch;
+    int32_t* cost = reinterpret_cast<int32_t*>(fz);
+    int64_t* pre = reinterpret_cast<int64_t*>(fz + fp.pre_off);
+    int32_t* bounds = reinterpret_cast<int32_t*>(fz + fp.bounds_off);
+    const int32_t* shr = shubs > 0 ? src_plan->hub_rank : nullptr;
+    k_tile_cost<<<unsigned(std::min<int64_t>((fp.nt + 255) / 256, 4096)), 256, 0, stream>>>(
+        colptr, shr, N, cost, amax);
+    GFD_LAUNCH_CHECK();
+    // max |g| per channel (the y-row scales); the column sums for grad_bias
+    k_colsum64<<<kRedBlocks, 256, 0, stream>>>(g, N, gbp, amax + kGOff);
+    GFD_LAUNCH_CHECK();
+    k_slab_bounds<<<1, 1024, 0, stream>>>(cost, fp.nt, fp.S, N, pre, bounds);
+    GFD_LAUNCH_CHECK();
+    const int Fu16 = (F + 15) / 16 * 16;
+    const size_t smem = size_t(flay(Fu16).bytes);
+    auto kern = xvec ? &k_src_gw<XT, true, 6> : &k_src_gw<XT, false, 6>;
+    if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
+    kern<<<unsigned(16 * ((fp.S + 7) / 8)), 512, smem, stream>>>(
+        colptr, csc_dst, csc_eid, shr, dh, alpha_d, dt, g, dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f,
+        x, ldx, F, Fu16, bounds, fp.S, amax, slab);
+    GFD_LAUNCH_CHECK();
+    const int64_t cols = int64_t(kDH) * F;
+    k_reduce_rows<<<unsigned((cols + 255) / 256), 256, 0, stream>>>(slab, fp.S, cols, cols, gw, 1);
+    GFD_LAUNCH_CHECK();
+    k_fold_gw<<<unsigned((int64_t(HC) * F + 255) / 256), 256, 0, stream>>>(gw, att_src, att_dst, F,
+                                                                          grad_W);
+    GFD_LAUNCH_CHECK();
+    k_att_grad<<<(2 * HC + 255) / 256, 256, 0, stream>>>(W, F, gw, grad_as, grad_ad);
+    GFD_LAUNCH_CHECK();
+  } else {
+    int64_t blocks = (N + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
     k_bwd_src<<<unsigned(blocks), 256, 0, stream>>>(
         colptr, csc_dst, csc_eid, N, shubs > 0 ? src_plan->hub_rank : nullptr, alpha_d, dpre, dt,
         g, att_src, att_dst, dh, amax, erow);
@@ -1421,19 +2086,16 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
       GFD_LAUNCH_CHECK();
       k_bwd_src_hub2<<<unsigned(shubs), 512, 0, stream>>>(spart, src_plan->hub_chunk_ptr,
                                                           src_plan->hub_dst, dt, att_src, att_dst,
-                                                          dh, amax, erow);
+                                                          dh, amax, erow, 0);
       GFD_LAUNCH_CHECK();
     }
-  }
-  // 4. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
-  {
+    // 4. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
     int64_t kps = (N + gw_slabs(N) - 1) / gw_slabs(N);
     kps = (kps + kGK - 1) / kGK * kGK;
     const int64_t z = (N + kps - 1) / kps;
     const int Fu16 = (F + 15) / 16 * 16;
     const size_t smem = gw_smem(Fu16);
-    const bool vec = ldx % 4 == 0 &&
-                     reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
+    const bool vec = xvec;
     auto kern = Fu16 <= 192 ? (vec ? &k_gw<XT, true, 6> : &k_gw<XT, false, 6>)
                             : (vec ? &k_gw<XT, true, 8> : &k_gw<XT, false, 8>);
     if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
@@ -1448,10 +2110,12 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
     k_att_grad<<<(2 * HC + 255) / 256, 256, 0, stream>>>(W, F, gw, grad_as, grad_ad);
     GFD_LAUNCH_CHECK();
   }
-  // 5. grad_bias = sum_i g_i
+  // 5. grad_bias = sum_i g_i (the fused path's k_colsum64 already ran)
   if (grad_bias) {
-    k_colsum64<<<kRedBlocks, 256, 0, stream>>>(g, N, gbp);
-    GFD_LAUNCH_CHECK();
+    if (fp.S == 0) {
+      k_colsum64<<<kRedBlocks, 256, 0, stream>>>(g, N, gbp, nullptr);
+      GFD_LAUNCH_CHECK();
+    }
     k_reduce_few<<<1, 1024, 0, stream>>>(gbp, kRedBlocks, 64, grad_bias);
     GFD_LAUNCH_CHECK();
   }
