@@ -1264,21 +1264,41 @@ __global__ void __launch_bounds__(512) k_src_gw(
   auto consume = [&](int n) {
     const int ln = opaque(lane);  // (LDS addresses recomputed, not pinned across the loop)
 #pragma unroll
-    for (int k = 0; k < kFCh; ++k) {
-      if (k < n) {
-        const int bb = k >> 3, kk = k & 7;
-        const int rk = __builtin_amdgcn_readlane(rr[bb], 8 * kk);
-        float* row = (head && rk == rfirst) ? hpw : yt + rk * kFYP;
-        const float gk = pg[bb][kk];
+    for (int bb = 0; bb < kFNB; ++bb) {
+      if (8 * bb < n) {
+        if (half == 0) {  // ds: one add per lane (slot lane >> 3, head lane & 7); half 1 has none
+          const int r = rr[bb];
+          if (r >= 0) add(((head && r == rfirst) ? hpw : yt + r * kFYP) + 256 + (ln & 7), pd[bb]);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          if (8 * bb + kk < n) {
+            const int rk = __builtin_amdgcn_readlane(rr[bb], 8 * kk);
+            float* row = (head && rk == rfirst) ? hpw : yt + rk * kFYP;
+            const float gk = pg[bb][kk];
+#pragma unroll
+            for (int hl = 0; hl < 4; ++hl)
+              add(row + hl * 64 + ln,
+                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa[bb]),
+                                                           8 * kk + 4 * half + hl)) * gk);
+          }
+        }
+      }
+    }
+  };
+  // source hubs among the wave's 4 nodes: their compact rows into the y tile
+  auto hub_rows = [&]() {
+    const int ln = opaque(lane);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 4 * wave + q;
+      const int cd = __builtin_amdgcn_readlane(code, r);
+      if (cd >= 0) {
+        const float* src = dhub + int64_t(cd) * kDH;
 #pragma unroll
         for (int hl = 0; hl < 4; ++hl)
-          add(row + hl * 64 + ln,
-              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa[bb]), 8 * kk + 4 * half + hl)) *
-                  gk);
-        if (half == 0) {  // ds (heads: lanes 0..7); half 1 forms no ds row
-          const float dsk = __shfl(pd[bb], 8 * kk + (lane & 7));
-          if (ln < 8) add(row + 256 + ln, dsk);
-        }
+          yt[r * kFYP + hl * 64 + ln] = src[256 * half + hl * 64 + ln];
+        if (half == 0 && ln < 8) yt[r * kFYP + 256 + ln] = src[HC + ln];
       }
     }
   };
@@ -1335,12 +1355,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
       const int k = 16 * kh + kk;
       const float yv = yt[k * kFYP + m];
       yt[k * kFYP + m] = 0.f;  // ready for the next tile's sums
-      v[kk] = hrk[k] == -1 ? yv : 0.f;
-    }
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {  // source hubs: their compact rows (rare)
-      const int cd = hrk[16 * kh + kk];
-      if (cd >= 0) v[kk] = dhub[int64_t(cd) * kDH + 256 * half + m];
+      v[kk] = hrk[k] >= -1 ? yv : 0.f;  // messages or a source hub's row
     }
     put_row(m, kh, v, ysc[m & 63]);
   };
@@ -1356,9 +1371,8 @@ __global__ void __launch_bounds__(512) k_src_gw(
       if (half) {
         val = cd == -2 ? 0.f : dtt[k * 8 + e];
       } else {
-        val = cd == -1 ? yt[k * kFYP + 256 + e] : 0.f;
+        val = cd >= -1 ? yt[k * kFYP + 256 + e] : 0.f;
         yt[k * kFYP + 256 + e] = 0.f;
-        if (cd >= 0) val = dhub[int64_t(cd) * kDH + HC + e];
       }
       v[kk] = val;
       mx = fmaxf(mx, fabsf(val));
@@ -1440,8 +1454,10 @@ __global__ void __launch_bounds__(512) k_src_gw(
         consume(min(hi - c, kFCh));
       }
     }
+    hub_rows();
     if (lane == 0) hpr[wave] = (lo < hi && head) ? rfirst : -1;
     __syncthreads();
+    store_x(opaque(tid));  // (B's last readers, the MFMAs, are behind the barrier)
     // ---- next tile's first chunk: prefix and indices ----
     if (t + 1 < T) prep(k0 + kFK);
     // ---- head partials into their owners' rows, in wave order (a fixed order) ----
@@ -1467,7 +1483,6 @@ __global__ void __launch_bounds__(512) k_src_gw(
     // ---- column pass ----
     {
       const int tq = opaque(tid);
-      store_x(tq);
       ycolumn(tq >> 1, tq & 1);
       if (tq < 16) xcolumn(tq >> 1, tq & 1);
     }
