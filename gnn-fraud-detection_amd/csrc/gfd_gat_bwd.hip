@@ -1109,8 +1109,8 @@ __host__ __device__ inline FLay flay(int Fu) {
   L.iax = take(16 * 4);
   L.csb = take(kGMaxF * 4);
   L.dtt = take(kFK * 8 * 4);
-  L.pw = take(8 * 33 * 4);
-  L.cw = take(8 * 32 * 4);
+  L.pw = take(2 * 8 * 33 * 4);  // per tile parity, per wave
+  L.cw = take(2 * 8 * 32 * 4);
   L.hrk = take(kFK * 4);
   L.hpr = take(8 * 4);
   L.bytes = o;
@@ -1167,13 +1167,14 @@ __global__ void __launch_bounds__(512) k_src_gw(
     Alo[kFE * kGPt + i] = _Float16(0.f);
   }
   if (tid >= 8 && tid < 16) iax[tid] = 0.f;
-  for (int i = tid; i < (kFK + 8) * kFYP; i += 512) yt[i] = 0.f;  // yt, hp adjacent
   __syncthreads();
 
-  int* P = pw + wave * 33;  // this wave's copy of the tile's message prefix
-  int* Cs = cw + wave * 32;  // and of its sources' CSC starts
+  // this wave's copies of a tile's message prefix and its sources' CSC starts,
+  // by tile parity (tile t + 1's are written during tile t's walk)
+  auto Pof = [&](int par) { return pw + (par * 8 + wave) * 33; };
+  auto Cof = [&](int par) { return cw + (par * 8 + wave) * 32; };
   // largest r in [0, 32) with P[r] <= f (P non-decreasing; f < P[32])
-  auto find = [&](int f) {
+  auto find = [](const int* P, int f) {
     int r = 0;
 #pragma unroll
     for (int st = 16; st >= 1; st >>= 1)
@@ -1182,12 +1183,17 @@ __global__ void __launch_bounds__(512) k_src_gw(
   };
 
   // --- per-wave pipeline state ---
-  int n_c0 = 0, n_c1 = 0, n_hr = -1;  // next tile: lane r's source colptr pair, hub rank
-  float n_dt = 0.f;                   // next tile: dt of node 4 wave + (lane >> 3), head lane & 7
-  int code = -2;                      // tile's lane r: hub rank | -1 | -2 outside | -3 no messages
-  int lo = 0, hi = 0, rfirst = 0;     // the wave's message range in the tile, its first source
-  bool head = false;                  // ... begun by an earlier wave
-  int pe[kFNB], pi[kFNB], rr[kFNB];   // chunk: edge ids, destinations, source per slot
+  int n_c0 = 0, n_c1 = 0, n_hr = -1;  // tile t + 2 (loaded during t): lane r's colptr pair, hub rank
+  float n_dt = 0.f;                   // tile t + 1: dt of node 4 wave + (lane >> 3), head lane & 7
+  // tile t's walk state (code: lane r's hub rank | -1 | -2 outside | -3 no messages;
+  // [lo, hi): the wave's message range, rfirst its first source, head: begun by an
+  // earlier wave) and tile t + 1's, prepared during tile t's walk (x_)
+  int code = -2, lo = 0, hi = 0, rfirst = 0;
+  bool head = false;
+  int x_code = -2, x_lo = 0, x_hi = 0, x_rf = 0;
+  bool x_head = false;
+  int pe[kFNB], pi[kFNB], rr[kFNB];       // chunk: edge ids, destinations, source per slot
+  int x_pe[kFNB], x_pi[kFNB], x_rr[kFNB];  // tile t + 1's first chunk
   float pa[kFNB], pd[kFNB], pg[kFNB][8];  // chunk: alpha~, dpre (lane 8 slot + head), g rows
 
   auto load_next = [&](int64_t k0) {
@@ -1196,19 +1202,22 @@ __global__ void __launch_bounds__(512) k_src_gw(
     n_c0 = colptr[jc];
     n_c1 = colptr[jc + 1];
     if (src_hub_rank) n_hr = src_hub_rank[jc];
+  };
+  auto load_dt = [&](int64_t k0) {
     const int64_t jd = k0 + 4 * wave + ((lane >> 3) & 3);
     n_dt = dt[(jd < ke ? jd : kb) * 8 + (lane & 7)];
   };
-  auto issue_idx = [&](int c) {
+  auto issue_idx = [&](const int* P, const int* Cs, int c, int h_end, int (&e_)[kFNB],
+                       int (&i_)[kFNB], int (&r_)[kFNB]) {
 #pragma unroll
     for (int bb = 0; bb < kFNB; ++bb) {
       const int f = c + 8 * bb + (lane >> 3);
-      const bool ok = f < hi;
-      const int r = find(ok ? f : c);
+      const bool ok = f < h_end;
+      const int r = find(P, ok ? f : c);
       const int p = ok ? Cs[r] + (f - P[r]) : 0;
-      pe[bb] = csc_eid[p];
-      pi[bb] = csc_dst[p];
-      rr[bb] = ok ? r : -1;
+      e_[bb] = csc_eid[p];
+      i_[bb] = csc_dst[p];
+      r_[bb] = ok ? r : -1;
     }
   };
   auto issue_data = [&]() {
@@ -1224,13 +1233,16 @@ __global__ void __launch_bounds__(512) k_src_gw(
       }
     }
   };
-  // the tile's prefix, the wave's range, and its first chunk's indices
-  auto prep = [&](int64_t k0) {
+  // tile k0's prefix (parity par), the wave's range, and its first chunk's
+  // indices, into the x_ state (from the n_ loads of a tile earlier)
+  auto prep = [&](int64_t k0, int par) {
+    int* P = Pof(par);
+    int* Cs = Cof(par);
     const int64_t j = k0 + (lane & 31);
     const bool in = lane < 32 && j < ke;
     const int hr = in ? n_hr : -2;
     const int d = (in && hr < 0) ? n_c1 - n_c0 : 0;
-    code = hr >= 0 ? hr : (hr == -2 ? -2 : (d > 0 ? -1 : -3));
+    x_code = hr >= 0 ? hr : (hr == -2 ? -2 : (d > 0 ? -1 : -3));
     int inc = d;
 #pragma unroll
     for (int off = 1; off < 32; off <<= 1) {
@@ -1243,46 +1255,64 @@ __global__ void __launch_bounds__(512) k_src_gw(
       Cs[lane] = n_c0;
     }
     if (lane == 0) P[32] = D;
-    lo = int((int64_t(wave) * D) >> 3);
-    hi = int((int64_t(wave + 1) * D) >> 3);
-    if (lo < hi) {
-      rfirst = __builtin_amdgcn_readfirstlane(find(lo));
-      head = lo > P[rfirst];
-      issue_idx(lo);
+    x_lo = int((int64_t(wave) * D) >> 3);
+    x_hi = int((int64_t(wave + 1) * D) >> 3);
+    if (x_lo < x_hi) {
+      x_rf = __builtin_amdgcn_readfirstlane(find(P, x_lo));
+      x_head = x_lo > P[x_rf];
+      issue_idx(P, Cs, x_lo, x_hi, x_pe, x_pi, x_rr);
     } else {
-      head = false;
+      x_head = false;
+    }
+  };
+  auto advance = [&]() {  // tile t + 1's prepared state becomes the current one
+    code = x_code;
+    lo = x_lo;
+    hi = x_hi;
+    rfirst = x_rf;
+    head = x_head;
+#pragma unroll
+    for (int bb = 0; bb < kFNB; ++bb) {
+      pe[bb] = x_pe[bb];
+      pi[bb] = x_pi[bb];
+      rr[bb] = x_rr[bb];
     }
   };
 
-  // accumulate a chunk's messages into the LDS rows: in program order, and no
-  // two waves ever add to the same row (owner rows vs head-partial rows), so the
-  // float sums have a fixed order.  Rows are zeroed by their readers.
+  // a chunk's messages, accumulated in registers (y: this half's 4 heads, lane =
+  // channel; ds: head lane, lanes 0..7) and flushed to the source's LDS row --
+  // or, for a source begun by an earlier wave, this wave's head-partial row --
+  // when the source changes.  (LDS float atomics instead: 5x slower, measured.)
   float* hpw = hp + wave * kFYP;
-  auto add = [](float* p, float v) {
-    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  int cur = 0;
+  float y[4], ds = 0.f;
+  auto flush = [&]() {
+    const int ln = opaque(lane);
+    float* row = (head && cur == rfirst) ? hpw : yt + cur * kFYP;
+#pragma unroll
+    for (int hl = 0; hl < 4; ++hl) row[hl * 64 + ln] = y[hl];
+    if (half == 0 && ln < 8) row[256 + ln] = ds;
   };
   auto consume = [&](int n) {
-    const int ln = opaque(lane);  // (LDS addresses recomputed, not pinned across the loop)
 #pragma unroll
-    for (int bb = 0; bb < kFNB; ++bb) {
-      if (8 * bb < n) {
-        if (half == 0) {  // ds: one add per lane (slot lane >> 3, head lane & 7); half 1 has none
-          const int r = rr[bb];
-          if (r >= 0) add(((head && r == rfirst) ? hpw : yt + r * kFYP) + 256 + (ln & 7), pd[bb]);
+    for (int k = 0; k < kFCh; ++k) {
+      if (k < n) {
+        const int bb = k >> 3, kk = k & 7;
+        const int rk = __builtin_amdgcn_readlane(rr[bb], 8 * kk);
+        if (rk != cur) {
+          flush();
+          cur = rk;
+#pragma unroll
+          for (int hl = 0; hl < 4; ++hl) y[hl] = 0.f;
+          ds = 0.f;
         }
+        const float gk = pg[bb][kk];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          if (8 * bb + kk < n) {
-            const int rk = __builtin_amdgcn_readlane(rr[bb], 8 * kk);
-            float* row = (head && rk == rfirst) ? hpw : yt + rk * kFYP;
-            const float gk = pg[bb][kk];
-#pragma unroll
-            for (int hl = 0; hl < 4; ++hl)
-              add(row + hl * 64 + ln,
-                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa[bb]),
-                                                           8 * kk + 4 * half + hl)) * gk);
-          }
-        }
+        for (int hl = 0; hl < 4; ++hl)
+          y[hl] = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa[bb]),
+                                                                8 * kk + 4 * half + hl)),
+                       gk, y[hl]);
+        if (half == 0) ds += __shfl(pd[bb], 8 * kk + (lane & 7));
       }
     }
   };
@@ -1354,7 +1384,6 @@ __global__ void __launch_bounds__(512) k_src_gw(
     for (int kk = 0; kk < 16; ++kk) {
       const int k = 16 * kh + kk;
       const float yv = yt[k * kFYP + m];
-      yt[k * kFYP + m] = 0.f;  // ready for the next tile's sums
       v[kk] = hrk[k] >= -1 ? yv : 0.f;  // messages or a source hub's row
     }
     put_row(m, kh, v, ysc[m & 63]);
@@ -1372,7 +1401,6 @@ __global__ void __launch_bounds__(512) k_src_gw(
         val = cd == -2 ? 0.f : dtt[k * 8 + e];
       } else {
         val = cd >= -1 ? yt[k * kFYP + 256 + e] : 0.f;
-        yt[k * kFYP + 256 + e] = 0.f;
       }
       v[kk] = val;
       mx = fmaxf(mx, fabsf(val));
@@ -1434,8 +1462,11 @@ __global__ void __launch_bounds__(512) k_src_gw(
   const int64_t T = (ke - kb + kFK - 1) / kFK;
   if (T > 0) {
     load_next(kb);
-    prep(kb);
+    load_dt(kb);
+    prep(kb, 0);
+    advance();
     if (lo < hi) issue_data();
+    if (T > 1) load_next(kb + kFK);
   }
   for (int64_t t = 0; t < T; ++t) {
     const int64_t k0 = kb + t * kFK;
@@ -1445,21 +1476,38 @@ __global__ void __launch_bounds__(512) k_src_gw(
       dtt[(4 * wave + (lane >> 3)) * 8 + (lane & 7)] =
           k0 + 4 * wave + (lane >> 3) < ke ? n_dt : 0.f;
     load_x(k0, opaque(tid));
-    if (t + 1 < T) load_next(k0 + kFK);
+    if (t + 1 < T) {
+      prep(k0 + kFK, int(t + 1) & 1);  // tile t + 1's first-chunk indices fly during this walk
+      load_dt(k0 + kFK);
+    }
+    if (t + 2 < T) load_next(k0 + 2 * kFK);
+#ifdef GFD_AB_F_NOY  // ablation: no y phase walk
+    if (false) {
+#else
     if (lo < hi) {
+#endif
+      cur = rfirst;
+#pragma unroll
+      for (int hl = 0; hl < 4; ++hl) y[hl] = 0.f;
+      ds = 0.f;
       consume(min(hi - lo, kFCh));
       for (int c = lo + kFCh; c < hi; c += kFCh) {  // long ranges: further chunks in place
-        issue_idx(c);
+        issue_idx(Pof(int(t) & 1), Cof(int(t) & 1), c, hi, pe, pi, rr);
         issue_data();
         consume(min(hi - c, kFCh));
       }
+      flush();
     }
     hub_rows();
     if (lane == 0) hpr[wave] = (lo < hi && head) ? rfirst : -1;
     __syncthreads();
+    // ---- tile t + 1's first chunk: records and g rows fly during this tile's
+    // column pass and MFMAs ----
+    if (t + 1 < T) {
+      advance();
+      if (lo < hi) issue_data();
+    }
     store_x(opaque(tid));  // (B's last readers, the MFMAs, are behind the barrier)
-    // ---- next tile's first chunk: prefix and indices ----
-    if (t + 1 < T) prep(k0 + kFK);
     // ---- head partials into their owners' rows, in wave order (a fixed order) ----
     {
       bool any = false;
@@ -1471,10 +1519,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
 #pragma unroll 1
           for (int w = 0; w < 8; ++w) {
             const int r = hpr[w];
-            if (r >= 0) {
-              yt[r * kFYP + tq] += hp[w * kFYP + tq];
-              hp[w * kFYP + tq] = 0.f;
-            }
+            if (r >= 0) yt[r * kFYP + tq] += hp[w * kFYP + tq];
           }
         }
         __syncthreads();
@@ -1483,13 +1528,16 @@ __global__ void __launch_bounds__(512) k_src_gw(
     // ---- column pass ----
     {
       const int tq = opaque(tid);
+#ifndef GFD_AB_F_NOCOL
       ycolumn(tq >> 1, tq & 1);
       if (tq < 16) xcolumn(tq >> 1, tq & 1);
+#endif
     }
     __syncthreads();
-    if (t + 1 < T && lo < hi) issue_data();
     // ---- MFMA ----
+#ifndef GFD_AB_F_NOMFMA
     mfma_tile();
+#endif
   }
 
   float* Cz = slab + int64_t(s) * kDH * F;
