@@ -1087,7 +1087,7 @@ constexpr int kFCost = 128;     // slab balance: a tile's fixed cost, in message
 constexpr int kFMaxFu = 192;    // the fused path's feature bound (NJ = 6)
 
 struct FLay {
-  int yt, hp, ahi, alo, bhi, blo, ysc, yinv, iax, csb, dtt, pw, cw, hrk, hpr, bytes;
+  int yt, hp, ahi, alo, bhi, blo, ysc, yinv, iax, csb, dtt, pw, cw, hpr, bytes;
 };
 
 __host__ __device__ inline FLay flay(int Fu) {
@@ -1111,7 +1111,6 @@ __host__ __device__ inline FLay flay(int Fu) {
   L.dtt = take(kFK * 8 * 4);
   L.pw = take(2 * 8 * 33 * 4);  // per tile parity, per wave
   L.cw = take(2 * 8 * 32 * 4);
-  L.hrk = take(kFK * 4);
   L.hpr = take(8 * 4);
   L.bytes = o;
   return L;
@@ -1140,7 +1139,6 @@ __global__ void __launch_bounds__(512) k_src_gw(
   float* dtt = reinterpret_cast<float*>(fsm + L.dtt);
   int* pw = reinterpret_cast<int*>(fsm + L.pw);
   int* cw = reinterpret_cast<int*>(fsm + L.cw);
-  int* hrk = reinterpret_cast<int*>(fsm + L.hrk);
   int* hpr = reinterpret_cast<int*>(fsm + L.hpr);
 
   const int b = blockIdx.x, rem = b & 15;
@@ -1221,6 +1219,9 @@ __global__ void __launch_bounds__(512) k_src_gw(
     }
   };
   auto issue_data = [&]() {
+#ifdef GFD_AB_F_NODATA  // ablation: no record / g-row gathers (garbage sums)
+    return;
+#endif
 #pragma unroll
     for (int bb = 0; bb < kFNB; ++bb) {
       const float* rp = rec + int64_t(pe[bb]) * kRec + (lane & 7);
@@ -1286,12 +1287,24 @@ __global__ void __launch_bounds__(512) k_src_gw(
   float* hpw = hp + wave * kFYP;
   int cur = 0;
   float y[4], ds = 0.f;
+  // ds of the current source from the chunk's (slot, head) lanes: sum over the
+  // lanes of each head whose slot holds one of its messages (every lane ends up
+  // with its head's sum)
+  auto chunk_ds = [&]() {
+    float d = 0.f;
+#pragma unroll
+    for (int bb = 0; bb < kFNB; ++bb) d += sum_xor8_16_32(rr[bb] == cur ? pd[bb] : 0.f);
+    return d;
+  };
   auto flush = [&]() {
     const int ln = opaque(lane);
     float* row = (head && cur == rfirst) ? hpw : yt + cur * kFYP;
 #pragma unroll
     for (int hl = 0; hl < 4; ++hl) row[hl * 64 + ln] = y[hl];
-    if (half == 0 && ln < 8) row[256 + ln] = ds;
+    if (half == 0) {
+      const float d = ds + chunk_ds();
+      if (ln < 8) row[256 + ln] = d;
+    }
   };
   auto consume = [&](int n) {
 #pragma unroll
@@ -1312,11 +1325,11 @@ __global__ void __launch_bounds__(512) k_src_gw(
           y[hl] = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa[bb]),
                                                                 8 * kk + 4 * half + hl)),
                        gk, y[hl]);
-        if (half == 0) ds += __shfl(pd[bb], 8 * kk + (lane & 7));
       }
     }
   };
-  // source hubs among the wave's 4 nodes: their compact rows into the y tile
+  // the wave's 4 nodes without messages: source hubs' compact rows into the y
+  // tile, zero rows for the rest
   auto hub_rows = [&]() {
     const int ln = opaque(lane);
 #pragma unroll
@@ -1329,6 +1342,10 @@ __global__ void __launch_bounds__(512) k_src_gw(
         for (int hl = 0; hl < 4; ++hl)
           yt[r * kFYP + hl * 64 + ln] = src[256 * half + hl * 64 + ln];
         if (half == 0 && ln < 8) yt[r * kFYP + 256 + ln] = src[HC + ln];
+      } else if (cd != -1) {  // outside the slab / no messages: a zero row
+#pragma unroll
+        for (int hl = 0; hl < 4; ++hl) yt[r * kFYP + hl * 64 + ln] = 0.f;
+        if (ln < 8) yt[r * kFYP + 256 + ln] = 0.f;
       }
     }
   };
@@ -1377,38 +1394,29 @@ __global__ void __launch_bounds__(512) k_src_gw(
     al[0] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
     al[1] = make_uint4(lv[4], lv[5], lv[6], lv[7]);
   };
-  // y column m (< 256) over nodes 16 kh .. 16 kh + 15 (partials merged)
+  // y column m (< 256) over nodes 16 kh .. 16 kh + 15 (partials merged; rows of
+  // sources without messages hold the hub row or zeros)
   auto ycolumn = [&](int m, int kh) {
     float v[16];
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      const int k = 16 * kh + kk;
-      const float yv = yt[k * kFYP + m];
-      v[kk] = hrk[k] >= -1 ? yv : 0.f;  // messages or a source hub's row
-    }
+    for (int kk = 0; kk < 16; ++kk) v[kk] = yt[(16 * kh + kk) * kFYP + m];
     put_row(m, kh, v, ysc[m & 63]);
   };
-  // ds (half 0) / dt (half 1) column e: the tile's exact max (lane pair)
-  auto xcolumn = [&](int e, int kh) {
-    float v[16];
-    float mx = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      const int k = 16 * kh + kk;
-      const int cd = hrk[k];
-      float val;
-      if (half) {
-        val = cd == -2 ? 0.f : dtt[k * 8 + e];
-      } else {
-        val = cd >= -1 ? yt[k * kFYP + 256 + e] : 0.f;
-      }
-      v[kk] = val;
-      mx = fmaxf(mx, fabsf(val));
+  // ds (half 0) / dt (half 1) column e (one per wave): lane k < 32 holds node k's
+  // value; the tile's exact max scales it
+  auto xcolumn = [&](int e) {
+    const int ln = opaque(lane);
+    const int k = ln & 31;
+    float val = half ? dtt[k * 8 + e] : yt[k * kFYP + 256 + e];
+    if (ln >= 32) val = 0.f;
+    const int ex = scale_exp(max_wave(fabsf(val)));
+    const float t = val * ldexpf(1.0f, ex);
+    const _Float16 h = _Float16(t);
+    if (ln < 32) {
+      Ahi[(256 + e) * kGPt + k] = h;
+      Alo[(256 + e) * kGPt + k] = _Float16(t - float(h));
     }
-    mx = fmaxf(mx, dpp_mov<0xB1>(mx));  // lane ^ 1: the column's other node half
-    const int ex = scale_exp(mx);
-    put_row(256 + e, kh, v, ldexpf(1.0f, ex));
-    if (kh == 0) iax[e] = ldexpf(1.0f, -ex);
+    if (ln == 0) iax[e] = ldexpf(1.0f, -ex);
   };
 
   f32x4 acc[4][NJ], accx[2];
@@ -1470,12 +1478,17 @@ __global__ void __launch_bounds__(512) k_src_gw(
   }
   for (int64_t t = 0; t < T; ++t) {
     const int64_t k0 = kb + t * kFK;
-    // ---- y phase ----
-    if (wave == 0 && lane < 32) hrk[lane] = code;
+    // ---- phase 1: tile t - 1's MFMAs (A / B images) overlapped with tile t's
+    // walk (the y tile): the walk's gathers wait behind the matrix cores ----
+#ifndef GFD_AB_F_NOMFMA
+    if (t > 0) mfma_tile();
+#endif
     if (lane < 32)
       dtt[(4 * wave + (lane >> 3)) * 8 + (lane & 7)] =
           k0 + 4 * wave + (lane >> 3) < ke ? n_dt : 0.f;
+#ifndef GFD_AB_F_NOX  // ablation: no x tile loads
     load_x(k0, opaque(tid));
+#endif
     if (t + 1 < T) {
       prep(k0 + kFK, int(t + 1) & 1);  // tile t + 1's first-chunk indices fly during this walk
       load_dt(k0 + kFK);
@@ -1491,7 +1504,12 @@ __global__ void __launch_bounds__(512) k_src_gw(
       for (int hl = 0; hl < 4; ++hl) y[hl] = 0.f;
       ds = 0.f;
       consume(min(hi - lo, kFCh));
+#ifdef GFD_AB_F_NOEXTRA  // ablation: first chunk only (wrong sums for long ranges)
+      for (int c = hi; c < hi; c += kFCh) {
+#else
       for (int c = lo + kFCh; c < hi; c += kFCh) {  // long ranges: further chunks in place
+#endif
+        if (half == 0) ds += chunk_ds();  // the running source's ds from this chunk
         issue_idx(Pof(int(t) & 1), Cof(int(t) & 1), c, hi, pe, pi, rr);
         issue_data();
         consume(min(hi - c, kFCh));
@@ -1501,8 +1519,8 @@ __global__ void __launch_bounds__(512) k_src_gw(
     hub_rows();
     if (lane == 0) hpr[wave] = (lo < hi && head) ? rfirst : -1;
     __syncthreads();
-    // ---- tile t + 1's first chunk: records and g rows fly during this tile's
-    // column pass and MFMAs ----
+    // ---- phase 2: tile t + 1's first chunk (records, g rows) flies during this
+    // tile's column pass and the next phase's MFMAs ----
     if (t + 1 < T) {
       advance();
       if (lo < hi) issue_data();
@@ -1530,15 +1548,14 @@ __global__ void __launch_bounds__(512) k_src_gw(
       const int tq = opaque(tid);
 #ifndef GFD_AB_F_NOCOL
       ycolumn(tq >> 1, tq & 1);
-      if (tq < 16) xcolumn(tq >> 1, tq & 1);
+      xcolumn(wave);
 #endif
     }
     __syncthreads();
-    // ---- MFMA ----
-#ifndef GFD_AB_F_NOMFMA
-    mfma_tile();
-#endif
   }
+#ifndef GFD_AB_F_NOMFMA
+  if (T > 0) mfma_tile();  // the last tile's
+#endif
 
   float* Cz = slab + int64_t(s) * kDH * F;
 #pragma unroll
@@ -1952,8 +1969,9 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
   return L;
 }
 
-// The fused source pass + grad_W' GEMM (k_src_gw) when grad_x is not
-// requested and F fits it; GFD_BWD_FUSED=0 selects the unfused dh' path (A/B).
+// The fused source pass + grad_W' GEMM (k_src_gw), opt-in with GFD_BWD_FUSED=1
+// when grad_x is not requested and F fits it.  Not the default: at C4 it runs
+// 23.9 ms against 21.5 ms for k_xmax + k_bwd_src + k_gw.
 // Its scratch (tile costs, their prefix, the slab bounds) follows the compact
 // hub rows in the dh region, which the fused pass does not otherwise use.
 struct FusedPlan {
@@ -1965,7 +1983,7 @@ struct FusedPlan {
 FusedPlan fused_plan(int64_t N, int F, int64_t shubs, bool want_gx) {
   FusedPlan p;
   const char* e = getenv("GFD_BWD_FUSED");
-  if (want_gx || (e && e[0] == '0') || (F + 15) / 16 * 16 > kFMaxFu) return p;
+  if (want_gx || !(e && e[0] == '1') || (F + 15) / 16 * 16 > kFMaxFu) return p;
   int64_t S = (N + 4095) / 4096;
   if (S > cu_count()) S = cu_count();
   if (S < 1) S = 1;
