@@ -36,8 +36,9 @@ constexpr int kLKS = 12;     // fp32 k-steps of 16 features (F <= 192)
 constexpr int kLKB = 6;      // f16 k-steps of 32 features
 
 // KS fp32 k-steps held per row (11: F <= 176, the f16 k-step 5 pairs step 10
-// with zeros; 12: F <= 192)
-template <typename XT, int KS>
+// with zeros; 12: F <= 192).  HEAD: the model head folded into the lone rows'
+// store (its own instance: the plain one stays inside 128 VGPRs, no spill)
+template <typename XT, int KS, bool HEAD>
 __global__ void __launch_bounds__(kLLWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_logits_lone(
     const typename XT::T* __restrict__ x, int64_t rows, int F, int64_t ldx,
@@ -182,7 +183,9 @@ k_logits_lone(
       sv[q] = acc[q] * (eq * uvu);
       const int64_t orow = t * 16 + src;
       // s | t columns of the row (sl / tl: separate tables, any strides)
-      if (orow < rows) (rl < H ? sl + uint64_t(orow) * lds : tl + uint64_t(orow) * ldt - H)[rl] = sv[q];
+      if (orow < rows)
+        (rl < H ? sl + uint64_t(uint32_t(orow)) * uint32_t(lds)
+                : tl + uint64_t(uint32_t(orow)) * uint32_t(ldt) - H)[rl] = sv[q];
     }
     if (!any_lone) continue;
     const int lone_i = lone ? 1 : 0;
@@ -196,7 +199,7 @@ k_logits_lone(
       const float tq = dpp_mov<0x128>(sv[q]);  // row_ror:8 within the 16-lane row
       if (lq) {  // uniform over the 16 lanes of the row (lane group g)
         const int64_t orow = t * 16 + src;
-        if (ep.hout) {  // model head: one dot per row instead of the row
+        if constexpr (HEAD) {  // model head: one dot per row instead of the row
           float d = 0.f;
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
@@ -206,9 +209,10 @@ k_logits_lone(
           d = row16_sum(d);
           if (rl == 0) ep.hout[orow] = d + (ep.hb ? ep.hb[0] : 0.f);
         } else {
+          float* orp = out + uint64_t(uint32_t(orow)) * uint32_t(ep.ldo) + rl;
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
-            out[orow * ep.ldo + ct * 16 + rl] =
+            orp[ct * 16] =
                 epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl,
                                 orow, ep);
         }
@@ -235,7 +239,8 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
   int64_t nb = (tiles + kLLWaves - 1) / kLLWaves;
   const int64_t cap = int64_t(cu_count()) * 2;  // resident blocks; grid-stride beyond
   if (nb > cap) nb = cap;
-  auto kern = F <= 176 ? &k_logits_lone<XT, 11> : &k_logits_lone<XT, 12>;
+  auto kern = ep.hout ? (F <= 176 ? &k_logits_lone<XT, 11, true> : &k_logits_lone<XT, 12, true>)
+                      : (F <= 176 ? &k_logits_lone<XT, 11, false> : &k_logits_lone<XT, 12, false>);
   const bool plain = XT::kBytes == 2;  // bf16: plain-order fragments (16-B loads)
   kern<<<int(nb), kLLWaves * 64, 0, stream>>>(
       static_cast<const typename XT::T*>(x), rows, F, ldx,
