@@ -213,13 +213,15 @@ def test_bf16_features_match_fp32_oracle_on_rounded_x(F):
     assert_close(out, _oracle(xb.float(), ei, W, a_s, a_d, b), what=f"bf16 x, F={F}")
 
 
-def test_c5_shape_bf16_sampled_parity():
+@pytest.mark.parametrize("row_align,ldx", [(16, 184), (128, 192)])
+def test_c5_shape_bf16_sampled_parity(row_align, ldx):
     """The C5 generator and layout (bf16 rows of 166 features + the 8-float
-    source-logit slot at byte 336: pitch 184) at 2M / 20M."""
+    source-logit slot at byte 336: pitch 184, or 192 on whole 128-B lines --
+    bench.py's C5 default) at 2M / 20M."""
     import bench
-    s = bench.setup(DEV, 2_000_000, 20_000_000, 166, dtype=torch.bfloat16)
+    s = bench.setup(DEV, 2_000_000, 20_000_000, 166, dtype=torch.bfloat16, row_align=row_align)
     s["bias"] = torch.randn(C, generator=torch.Generator().manual_seed(2)).to(DEV) * 0.1
-    assert s["ldx"] == 184 and s["x"].dtype == torch.bfloat16 and s["s_row"] == (84, 92)
+    assert s["ldx"] == ldx and s["x"].dtype == torch.bfloat16 and s["s_row"] == (84, ldx // 2)
     layer = bench.Layer(s, DEV, 1)
     assert layer.in_row
     layer.step()
