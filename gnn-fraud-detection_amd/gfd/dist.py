@@ -415,8 +415,76 @@ def gather_hidden(table: torch.Tensor, next_conv, spec: ShardSpec, group=None):
     return table[:n, :C], LogitsTable(table[:n, C:], st_l[:, H:]), xmax, packed
 
 
+class _SubSpec:
+    """Destinations [lo, hi) of a rank's block, as _aggregate reads a spec."""
+
+    def __init__(self, spec: ShardSpec, lo: int, hi: int):
+        self.rank, self.world, self.num_nodes = spec.rank, spec.world, spec.num_nodes
+        self.dst_lo, self.dst_hi = lo, hi
+
+
+def layer_forward_gather_overlapped(conv, bn, h: torch.Tensor, graph, spec: ShardSpec,
+                                    residual: bool, group, st, xmax, packed,
+                                    table: torch.Tensor, next_conv, chunks: int = 4):
+    """A hidden layer body fused with the exchange before the next layer, the
+    collective overlapped with the aggregation (SURVEY.md §8e "Expected
+    scaling"; equal node blocks).  The rank's destinations go in ``chunks``
+    pieces: piece c is aggregated into its rows of the ``[rows, 72]`` exchange
+    table, the next layer's logits of those rows are computed (s into columns
+    64..71), and piece c of EVERY rank is all-gathered asynchronously (RCCL's
+    own stream) while piece c + 1 is aggregated on the compute stream; every
+    piece's collective is waited for at the end.  Returns what gather_hidden
+    returns.  Same values as layer_forward_sharded + gather_hidden: the pieces
+    are the same rows through the same kernels."""
+    import torch.distributed as dist
+    from .fused import bn_affine
+    H, C = 8, 64
+    dev = h.device
+    if packed is None:
+        packed = pack_weights(conv.lin_src.weight.detach(), conv.att_src.detach(),
+                              conv.att_dst.detach())
+    if st is None:
+        xmax = torch.zeros(1, dtype=torch.float32, device=dev)
+        st = exchange_logits(h, packed, spec, xmax, group=group)
+        dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
+    st = _as_table(st, spec)
+    next_packed = pack_weights(next_conv.lin_src.weight.detach(), next_conv.att_src.detach(),
+                               next_conv.att_dst.detach())
+    bias = conv.bias.detach() if conv.bias is not None else None
+    aff = bn_affine(bn, dev)
+    per, w, r = spec.per, spec.world, spec.rank
+    n_own = spec.dst_hi - spec.dst_lo
+    cs = max((per + chunks - 1) // chunks, 1)
+    next_xmax = torch.zeros(1, dtype=torch.float32, device=dev)
+    st_own = torch.empty((max(n_own, 0), 2 * H), dtype=torch.float32, device=dev)
+    works = []
+    for c0 in range(0, per, cs):
+        c1 = min(c0 + cs, per)
+        lo, hi = min(spec.dst_lo + c0, spec.dst_hi), min(spec.dst_lo + c1, spec.dst_hi)
+        if hi > lo:   # the last rank's block may end before its padded rows
+            sub = _SubSpec(spec, lo, hi)
+            res = None
+            if residual:
+                res = h[lo:hi]
+                res = res if res.dtype == torch.float32 else res.float()
+            piece = table[lo:hi]
+            shard_aggregate_ep(h, graph, LogitsTable(st.s, st.t[lo - spec.dst_lo:hi - spec.dst_lo]),
+                               packed, bias, sub, conv.negative_slope, xmax, aff, True, res,
+                               out=piece[:, :C])
+            st_l = logits_rows(piece[:, :C], next_packed, 0, hi - lo, next_xmax)
+            piece[:, C:] = st_l[:, :H]
+            st_own[lo - spec.dst_lo:hi - spec.dst_lo] = st_l
+        views = [table[q * per + c0:q * per + c1] for q in range(w)]
+        works.append(dist.all_gather(views, views[r], group=group, async_op=True))
+    for wk in works:
+        wk.wait()
+    dist.all_reduce(next_xmax, op=dist.ReduceOp.MAX, group=group)
+    n = spec.num_nodes
+    return table[:n, :C], LogitsTable(table[:n, C:], st_own[:, H:]), next_xmax, next_packed
+
+
 def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=None,
-                          gather_output: bool = True):
+                          gather_output: bool = True, overlap_chunks: int = 4):
     """Destination-sharded eval forward of gfd.models.GAT / TemporalGNN (the
     reference's 2-3 layer stacks, gat.py:60-96, tgn.py:67-113) on this rank.
 
@@ -438,9 +506,15 @@ def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=
         res = model.residual and h.size(-1) == model.hidden_channels
         if layer < L - 1 and spec.world > 1:
             table = exchange_table(HID, spec, x.device)
-            layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed,
-                                  out=own_block(table, spec)[:, :64])
-            h, st, xmax, packed = gather_hidden(table, model.gat_layers[layer + 1], spec, group)
+            nxt = model.gat_layers[layer + 1]
+            if spec.equal_blocks() and overlap_chunks > 1:   # collective under the compute
+                h, st, xmax, packed = layer_forward_gather_overlapped(
+                    conv, bn, h, graph, spec, res, group, st, xmax, packed, table, nxt,
+                    overlap_chunks)
+            else:
+                layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed,
+                                      out=own_block(table, spec)[:, :64])
+                h, st, xmax, packed = gather_hidden(table, nxt, spec, group)
         else:
             h = layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed)
             st = xmax = packed = None

@@ -97,7 +97,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, q, balance="messages"):
+def _rank_main(rank, world, port, q, balance="messages", chunks=4):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "gnn-fraud-detection_amd")):
@@ -113,22 +113,26 @@ def _rank_main(rank, world, port, q, balance="messages"):
         rowptr, col = csr_cpu(ei, N)
         spec = gdist.ShardSpec(rowptr, rank, world, balance)
         with torch.no_grad():
-            out = gdist.model_forward_sharded(m, x, (rowptr, col), spec)
+            out = gdist.model_forward_sharded(m, x, (rowptr, col), spec, overlap_chunks=chunks)
         if rank == 0:
             q.put(out)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,balance", [(2, "messages"), (3, "messages"), (4, "messages"),
-                                           (3, "nodes"), (4, "nodes")])
-def test_model_sharded_orchestration_gloo(world, balance):
+@pytest.mark.parametrize("world,balance,chunks", [
+    (2, "messages", 4), (3, "messages", 4), (4, "messages", 4),
+    (3, "nodes", 1), (4, "nodes", 1),       # hidden exchange after the layer (gather_hidden)
+    (3, "nodes", 4), (4, "nodes", 3)])      # overlapped with the layer, in pieces
+def test_model_sharded_orchestration_gloo(world, balance, chunks):
     """balance "nodes": equal blocks, every exchange one in-place all-gather
-    into the layer's table; "messages": uneven blocks (gloo's padded path)."""
+    into the layer's table -- or, before a hidden layer, ``chunks`` pieces
+    all-gathered asynchronously under the aggregation of the next piece;
+    "messages": uneven blocks (gloo's padded path)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _store_path()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, balance))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, balance, chunks))
              for r in range(world)]
     for p in procs:
         p.start()
