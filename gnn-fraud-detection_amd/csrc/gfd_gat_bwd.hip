@@ -1116,6 +1116,15 @@ __host__ __device__ inline FLay flay(int Fu) {
   return L;
 }
 
+#ifdef GFD_FPROF
+// Diagnostic build only (GFD_BUILD_VARIANT=fprof GFD_EXTRA_FLAGS=-DGFD_FPROF):
+// per-wave s_memtime cycles of k_src_gw's tile loop phases, summed over waves:
+// 0 MFMA(t - 1), 1 prefix / loads issue, 2 walk (consume, flush), 3 hub rows +
+// barrier A, 6 next data issue, 7 x tile to B, 4 merge, 5 column pass +
+// barrier B; [8] tiles (waves x tiles).  Read by gfd_fprof_read (scripts/prof_fused_bwd.py).
+__device__ unsigned long long g_fprof[10];
+#endif
+
 template <typename XT, bool VEC, int NJ>
 __global__ void __launch_bounds__(512) k_src_gw(
     const int32_t* __restrict__ colptr, const int32_t* __restrict__ csc_dst,
@@ -1244,12 +1253,14 @@ __global__ void __launch_bounds__(512) k_src_gw(
     const int hr = in ? n_hr : -2;
     const int d = (in && hr < 0) ? n_c1 - n_c0 : 0;
     x_code = hr >= 0 ? hr : (hr == -2 ? -2 : (d > 0 ? -1 : -3));
+    // inclusive scan over lanes 0..31 on DPP (no LDS round trips): shifts
+    // 1, 2, 4, 8 inside each 16-lane row, then row 1 += lane 15 (row_bcast:15)
     int inc = d;
-#pragma unroll
-    for (int off = 1; off < 32; off <<= 1) {
-      const int t = __shfl_up(inc, off);
-      if (lane >= off) inc += t;
-    }
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xF, 0xF, false);  // row_shr:1
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xF, 0xF, false);  // row_shr:2
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xF, 0xF, false);  // row_shr:4
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xF, 0xF, false);  // row_shr:8
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xA, 0xF, false);  // row_bcast:15
     const int D = __builtin_amdgcn_readlane(inc, 31);
     if (lane < 32) {
       P[lane] = inc - d;
@@ -1396,7 +1407,15 @@ __global__ void __launch_bounds__(512) k_src_gw(
   };
   // y column m (< 256) over nodes 16 kh .. 16 kh + 15 (partials merged; rows of
   // sources without messages hold the hub row or zeros)
-  auto ycolumn = [&](int m, int kh) {
+  // hw[w]: the source of wave w's head-partial row (-1: none), wave order
+  auto ycolumn = [&](int m, int kh, const int (&hw)[8]) {
+    // the partials of this thread's nodes first, in wave order (a fixed order;
+    // the same thread reads the sums back: no barrier)
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const int r = hw[w];
+      if (r >= 16 * kh && r < 16 * kh + 16) yt[r * kFYP + m] += hp[w * kFYP + m];
+    }
     float v[16];
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) v[kk] = yt[(16 * kh + kk) * kFYP + m];
@@ -1404,10 +1423,15 @@ __global__ void __launch_bounds__(512) k_src_gw(
   };
   // ds (half 0) / dt (half 1) column e (one per wave): lane k < 32 holds node k's
   // value; the tile's exact max scales it
-  auto xcolumn = [&](int e) {
+  auto xcolumn = [&](int e, const int (&hw)[8]) {
     const int ln = opaque(lane);
     const int k = ln & 31;
     float val = half ? dtt[k * 8 + e] : yt[k * kFYP + 256 + e];
+    if (!half) {  // ds partials of node k, in wave order
+#pragma unroll
+      for (int w = 0; w < 8; ++w)
+        if (hw[w] == k) val += hp[w * kFYP + 256 + e];
+    }
     if (ln >= 32) val = 0.f;
     const int ex = scale_exp(max_wave(fabsf(val)));
     const float t = val * ldexpf(1.0f, ex);
@@ -1476,6 +1500,20 @@ __global__ void __launch_bounds__(512) k_src_gw(
     if (lo < hi) issue_data();
     if (T > 1) load_next(kb + kFK);
   }
+#ifdef GFD_FPROF
+  unsigned long long pc[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+  unsigned long long ts = __builtin_amdgcn_s_memtime();
+#define GFD_FSTAMP(i)                                           \
+  do {                                                          \
+    const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
+    pc[i] += tn - ts;                                           \
+    ts = tn;                                                    \
+  } while (0)
+#else
+#define GFD_FSTAMP(i) \
+  do {                \
+  } while (0)
+#endif
   for (int64_t t = 0; t < T; ++t) {
     const int64_t k0 = kb + t * kFK;
     // ---- phase 1: tile t - 1's MFMAs (A / B images) overlapped with tile t's
@@ -1483,17 +1521,19 @@ __global__ void __launch_bounds__(512) k_src_gw(
 #ifndef GFD_AB_F_NOMFMA
     if (t > 0) mfma_tile();
 #endif
+    GFD_FSTAMP(0);
     if (lane < 32)
       dtt[(4 * wave + (lane >> 3)) * 8 + (lane & 7)] =
           k0 + 4 * wave + (lane >> 3) < ke ? n_dt : 0.f;
-#ifndef GFD_AB_F_NOX  // ablation: no x tile loads
-    load_x(k0, opaque(tid));
-#endif
     if (t + 1 < T) {
       prep(k0 + kFK, int(t + 1) & 1);  // tile t + 1's first-chunk indices fly during this walk
       load_dt(k0 + kFK);
     }
     if (t + 2 < T) load_next(k0 + 2 * kFK);
+#ifndef GFD_AB_F_NOX  // ablation: no x tile loads
+    load_x(k0, opaque(tid));
+#endif
+    GFD_FSTAMP(1);
 #ifdef GFD_AB_F_NOY  // ablation: no y phase walk
     if (false) {
 #else
@@ -1516,46 +1556,46 @@ __global__ void __launch_bounds__(512) k_src_gw(
       }
       flush();
     }
+    GFD_FSTAMP(2);
     hub_rows();
     if (lane == 0) hpr[wave] = (lo < hi && head) ? rfirst : -1;
     __syncthreads();
+    GFD_FSTAMP(3);
     // ---- phase 2: tile t + 1's first chunk (records, g rows) flies during this
     // tile's column pass and the next phase's MFMAs ----
     if (t + 1 < T) {
       advance();
       if (lo < hi) issue_data();
     }
+    GFD_FSTAMP(6);
     store_x(opaque(tid));  // (B's last readers, the MFMAs, are behind the barrier)
-    // ---- head partials into their owners' rows, in wave order (a fixed order) ----
-    {
-      bool any = false;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) any |= hpr[w] >= 0;
-      if (any) {  // block-uniform
-        const int tq = opaque(tid);
-        if (tq < kFE) {
-#pragma unroll 1
-          for (int w = 0; w < 8; ++w) {
-            const int r = hpr[w];
-            if (r >= 0) yt[r * kFYP + tq] += hp[w * kFYP + tq];
-          }
-        }
-        __syncthreads();
-      }
-    }
-    // ---- column pass ----
+    GFD_FSTAMP(7);
+    GFD_FSTAMP(4);
+    // ---- column pass (head partials merged by the threads that read them) ----
     {
       const int tq = opaque(tid);
+      int hw[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) hw[w] = __builtin_amdgcn_readfirstlane(hpr[w]);
 #ifndef GFD_AB_F_NOCOL
-      ycolumn(tq >> 1, tq & 1);
-      xcolumn(wave);
+      ycolumn(tq >> 1, tq & 1, hw);
+      xcolumn(wave, hw);
 #endif
     }
     __syncthreads();
+    GFD_FSTAMP(5);
   }
 #ifndef GFD_AB_F_NOMFMA
   if (T > 0) mfma_tile();  // the last tile's
 #endif
+#ifdef GFD_FPROF
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_fprof[i], pc[i]);
+    atomicAdd(&g_fprof[8], (unsigned long long)T);
+  }
+#endif
+#undef GFD_FSTAMP
 
   float* Cz = slab + int64_t(s) * kDH * F;
 #pragma unroll
@@ -2271,3 +2311,14 @@ gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ld
 }
 
 }  // extern "C"
+
+#ifdef GFD_FPROF
+extern "C" int gfd_fprof_read(unsigned long long* out10, int reset) {
+  if (hipMemcpyFromSymbol(out10, HIP_SYMBOL(g_fprof), sizeof(g_fprof)) != hipSuccess) return 1;
+  if (reset) {
+    static const unsigned long long zero[10] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_fprof), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
