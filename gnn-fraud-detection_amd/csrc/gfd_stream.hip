@@ -64,6 +64,21 @@ template <bool LIGHT, typename XT>
 constexpr int ap_of() {
   return LIGHT ? (XT::kBytes == 2 ? GFD_LIGHT_AP_BF16 : GFD_LIGHT_AP) : GFD_GENERAL_AP;
 }
+// x rows of a general slot issued one tile ahead (the rest of batch 0 is
+// issued when its aggregation starts).  fp32 rows: none -- the kernel is then
+// spill-free and C4's general stage 3.13 -> 3.00 ms; bf16 rows: 4 (without them
+// C5's general stage 35.8 -> 56.2 ms: the half-size rows issued during the MFMA
+// phase hide most of a round trip)
+#ifndef GFD_GENERAL_NL_F32
+#define GFD_GENERAL_NL_F32 0
+#endif
+#ifndef GFD_GENERAL_NL_BF16
+#define GFD_GENERAL_NL_BF16 4
+#endif
+template <bool LIGHT, typename XT>
+constexpr int nl_of() {
+  return LIGHT ? kLightMax : (XT::kBytes == 2 ? GFD_GENERAL_NL_BF16 : GFD_GENERAL_NL_F32);
+}
 
 #ifdef GFD_PROF
 // Diagnostic build only (GFD_BUILD_VARIANT=prof GFD_EXTRA_FLAGS=-DGFD_PROF):
@@ -224,9 +239,9 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLight
 //    the end of the current one (one memory round trip per batch; a col ->
 //    st -> rows chain would be three).
 //  * hub rows: the merged, normalised z of k_hub_fin.
-template <typename XT, int KF>
+template <typename XT, int KF, int NRW, int NRA>
 __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
-                                           const SlotRows<KF>& q, const void* __restrict__ x,
+                                           const SlotRows<KF, NRA>& q, const void* __restrict__ x,
                                            int64_t ldx, int F, int Fp,
                                            const int32_t* __restrict__ col,
                                            const float* __restrict__ s, int lds, float slope, float dp,
@@ -259,14 +274,31 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
     const float keep = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
     float m, l;
     {  // batch 0
+      if constexpr (NRW == 0) {  // rows 0..7 issued here, before the softmax
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * k), ldx), F, lane, k < n,
+                           xa[k]);
+        if (n > 4) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), ldx), F,
+                             lane, 4 + k < n, xb[k]);
+        }
+      }
       const bool valid = kk < n;
       const float v = leaky01(q.sj + q.th, slope);
       m = max_xor8_16_32(valid ? v : -INFINITY);
       float pv = valid ? __expf(v - m) : 0.f;
       l = pv;
       if (dp > 0.f) pv = dropout_keep(seed, uint32_t(e0 + kk), uint32_t(h), dp) ? pv * keep : 0.f;
-      fma_rows<KF, 4>(z, q.xv, pv, 0, min(4, n));
-      if (n > 4) {  // rows 4..7
+      if constexpr (NRW == 0) {
+        fma_rows<KF, 4>(z, xa, pv, 0, min(4, n));
+        if (n > 4) fma_rows<KF, 4>(z, xb, pv, 4, min(4, n - 4));
+      } else {
+        fma_rows<KF, 4>(z, q.xv, pv, 0, min(4, n));
+      }
+      if (NRW > 0 && n > 4) {  // rows 4..7
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), ldx), F, lane,
@@ -409,25 +441,24 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   if (nv == 0) return;  // uniform per block: no barrier below is reached by anyone
 
   SlotRec n0, n1;
-  constexpr int NL = LIGHT ? kLightMax : 4;  // rows issued one tile ahead per slot
-  SlotRows<KF, NL> d0, d1;
+  constexpr int NL = nl_of<LIGHT, XT>();  // rows issued one tile ahead per slot
+  constexpr int NA = NL > 0 ? NL : 1;      // (register arrays of at least one row)
+  SlotRows<KF, NA> d0, d1;
   // prologue: tile 0 issued and aggregated; records of tile 1 loading
   sl_rec(n0, slot(0, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(0, r1), num_dst, lim, desc, cols8, lane);
 #define GFD_ISSUE(P, n, d, ring) \
   sl_issue_part<P, XT, KF, LIGHT>(n, d, x, ldx, F, col, s, lds, t, ldt, ring, lane)
-  GFD_ISSUE(0, n0, d0, ring0 + r0); GFD_ISSUE(1, n0, d0, ring0 + r0);
-  GFD_ISSUE(2, n0, d0, ring0 + r0); GFD_ISSUE(3, n0, d0, ring0 + r0);
-  GFD_ISSUE(4, n0, d0, ring0 + r0);
-  if constexpr (NL >= 5) GFD_ISSUE((NL >= 5 ? 5 : 4), n0, d0, ring0 + r0);
-  if constexpr (NL >= 6) GFD_ISSUE((NL >= 6 ? 6 : 4), n0, d0, ring0 + r0);
-  if constexpr (NL >= 7) GFD_ISSUE((NL >= 7 ? 7 : 4), n0, d0, ring0 + r0);
-  GFD_ISSUE(0, n1, d1, ring0 + r1); GFD_ISSUE(1, n1, d1, ring0 + r1);
-  GFD_ISSUE(2, n1, d1, ring0 + r1); GFD_ISSUE(3, n1, d1, ring0 + r1);
-  GFD_ISSUE(4, n1, d1, ring0 + r1);
-  if constexpr (NL >= 5) GFD_ISSUE((NL >= 5 ? 5 : 4), n1, d1, ring0 + r1);
-  if constexpr (NL >= 6) GFD_ISSUE((NL >= 6 ? 6 : 4), n1, d1, ring0 + r1);
-  if constexpr (NL >= 7) GFD_ISSUE((NL >= 7 ? 7 : 4), n1, d1, ring0 + r1);
+#define GFD_ROW(k, n, d, ring) \
+  if constexpr (NL >= k) GFD_ISSUE((NL >= k ? k : 0), n, d, ring)
+  GFD_ISSUE(0, n0, d0, ring0 + r0);
+  GFD_ROW(1, n0, d0, ring0 + r0); GFD_ROW(2, n0, d0, ring0 + r0); GFD_ROW(3, n0, d0, ring0 + r0);
+  GFD_ROW(4, n0, d0, ring0 + r0); GFD_ROW(5, n0, d0, ring0 + r0); GFD_ROW(6, n0, d0, ring0 + r0);
+  GFD_ROW(7, n0, d0, ring0 + r0);
+  GFD_ISSUE(0, n1, d1, ring0 + r1);
+  GFD_ROW(1, n1, d1, ring0 + r1); GFD_ROW(2, n1, d1, ring0 + r1); GFD_ROW(3, n1, d1, ring0 + r1);
+  GFD_ROW(4, n1, d1, ring0 + r1); GFD_ROW(5, n1, d1, ring0 + r1); GFD_ROW(6, n1, d1, ring0 + r1);
+  GFD_ROW(7, n1, d1, ring0 + r1);
   sl_rec(n0, slot(1, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, lim, desc, cols8, lane);
   auto aggregate = [&](int tpar) {  // this wave's two slots of the tile in parity tpar
@@ -442,10 +473,10 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       sl_light<KF>(db, d1, kmax, slope, dp, seed, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid,
                    r1, erg, lane);
     } else {
-      sl_general<XT, KF>(rg + r0, d0, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub, stats,
-                         Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane);
-      sl_general<XT, KF>(rg + r1, d1, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub, stats,
-                         Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg, lane);
+      sl_general<XT, KF, NL, NA>(rg + r0, d0, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
+                                 stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane);
+      sl_general<XT, KF, NL, NA>(rg + r1, d1, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
+                                 stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg, lane);
     }
   };
   aggregate(0);
@@ -530,23 +561,20 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       // rows) spread evenly, piece i in k-step i * KHM / (2 NL + 2)
       SlotRing* rg = ring0 + pn * kTile;
 #define GFD_PIECE(i) (u == (i) * KHM / (2 * NL + 2))
+#define GFD_PROW(i, k, n, d, ring) \
+  if constexpr (NL >= k) if (GFD_PIECE(i)) GFD_ISSUE((NL >= k ? k : 0), n, d, ring)
       if (GFD_PIECE(0)) GFD_ISSUE(0, n0, d0, rg + r0);
-      if (GFD_PIECE(1)) GFD_ISSUE(1, n0, d0, rg + r0);
-      if (GFD_PIECE(2)) GFD_ISSUE(2, n0, d0, rg + r0);
-      if (GFD_PIECE(3)) GFD_ISSUE(3, n0, d0, rg + r0);
-      if (GFD_PIECE(4)) GFD_ISSUE(4, n0, d0, rg + r0);
-      if constexpr (NL >= 5) if (GFD_PIECE(5)) GFD_ISSUE((NL >= 5 ? 5 : 4), n0, d0, rg + r0);
-      if constexpr (NL >= 6) if (GFD_PIECE(6)) GFD_ISSUE((NL >= 6 ? 6 : 4), n0, d0, rg + r0);
-      if constexpr (NL >= 7) if (GFD_PIECE(7)) GFD_ISSUE((NL >= 7 ? 7 : 4), n0, d0, rg + r0);
+      GFD_PROW(1, 1, n0, d0, rg + r0); GFD_PROW(2, 2, n0, d0, rg + r0);
+      GFD_PROW(3, 3, n0, d0, rg + r0); GFD_PROW(4, 4, n0, d0, rg + r0);
+      GFD_PROW(5, 5, n0, d0, rg + r0); GFD_PROW(6, 6, n0, d0, rg + r0);
+      GFD_PROW(7, 7, n0, d0, rg + r0);
       if (GFD_PIECE(NL)) sl_rec(n0, slot(v + 2, r0), num_dst, lim, desc, cols8, lane);
       if (GFD_PIECE(NL + 1)) GFD_ISSUE(0, n1, d1, rg + r1);
-      if (GFD_PIECE(NL + 2)) GFD_ISSUE(1, n1, d1, rg + r1);
-      if (GFD_PIECE(NL + 3)) GFD_ISSUE(2, n1, d1, rg + r1);
-      if (GFD_PIECE(NL + 4)) GFD_ISSUE(3, n1, d1, rg + r1);
-      if (GFD_PIECE(NL + 5)) GFD_ISSUE(4, n1, d1, rg + r1);
-      if constexpr (NL >= 5) if (GFD_PIECE(NL + 6)) GFD_ISSUE((NL >= 5 ? 5 : 4), n1, d1, rg + r1);
-      if constexpr (NL >= 6) if (GFD_PIECE(NL + 7)) GFD_ISSUE((NL >= 6 ? 6 : 4), n1, d1, rg + r1);
-      if constexpr (NL >= 7) if (GFD_PIECE(NL + 8)) GFD_ISSUE((NL >= 7 ? 7 : 4), n1, d1, rg + r1);
+      GFD_PROW(NL + 2, 1, n1, d1, rg + r1); GFD_PROW(NL + 3, 2, n1, d1, rg + r1);
+      GFD_PROW(NL + 4, 3, n1, d1, rg + r1); GFD_PROW(NL + 5, 4, n1, d1, rg + r1);
+      GFD_PROW(NL + 6, 5, n1, d1, rg + r1); GFD_PROW(NL + 7, 6, n1, d1, rg + r1);
+      GFD_PROW(NL + 8, 7, n1, d1, rg + r1);
+#undef GFD_PROW
       if (GFD_PIECE(2 * NL + 1)) sl_rec(n1, slot(v + 2, r1), num_dst, lim, desc, cols8, lane);
 #undef GFD_PIECE
       if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
@@ -605,6 +633,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     atomicAdd(&g_prof[LIGHT ? 1 : 0][5], pc[4]);
   }
 #endif
+#undef GFD_ROW
 #undef GFD_ISSUE
   if (!kh) reduce_store(acc_prev, int((nv - 1) & 1));  // last tile
   if (ep.hout) {  // kernel-uniform
