@@ -50,6 +50,7 @@ k_logits_lone(
     float* __restrict__ stats, Epi ep) {
   __shared__ uint4 WB[2][kLKB][4][64];  // permuted Wbar hi / lo fragments, zero past KB
   __shared__ uint4 UP[2][kLKB][64];     // permuted [U | V] hi / lo fragments, zero past KB
+  __shared__ float BH[2][C];            // bias and (HEAD) head weights for the launch
   const int KB = (F + 31) / 32;
   const int kst = (F + 15) / 16;  // fp32 k-steps incl. the ragged tail
   const int ksf = F / 16;         // fp32 k-steps fully inside the row
@@ -62,6 +63,10 @@ k_logits_lone(
     const bool in = i < KB * 64;
     UP[0][0][i] = in ? uph[i] : make_uint4(0, 0, 0, 0);
     UP[1][0][i] = in ? upl[i] : make_uint4(0, 0, 0, 0);
+  }
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    BH[0][i] = bias ? bias[i] : 0.f;
+    BH[1][i] = HEAD ? ep.hw[i] : 0.f;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -203,9 +208,8 @@ k_logits_lone(
           float d = 0.f;
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
-            d = fmaf(epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl,
-                                     orow, ep),
-                     ep.hw[ct * 16 + rl], d);
+            d = fmaf(epi_store_value(o[ct][q] * uq, BH[0][ct * 16 + rl], ct * 16 + rl, orow, ep),
+                     BH[1][ct * 16 + rl], d);
           d = row16_sum(d);
           if (rl == 0) ep.hout[orow] = d + (ep.hb ? ep.hb[0] : 0.f);
         } else {
@@ -213,7 +217,7 @@ k_logits_lone(
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
             orp[ct * 16] =
-                epi_store_value(o[ct][q] * uq, bias ? bias[ct * 16 + rl] : 0.f, ct * 16 + rl,
+                epi_store_value(o[ct][q] * uq, BH[0][ct * 16 + rl], ct * 16 + rl,
                                 orow, ep);
         }
         if (__builtin_expect(stats != nullptr, 0) && rl < H) {  // training (no dropout) only
