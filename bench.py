@@ -65,6 +65,10 @@ def parse(argv=None):
     p.add_argument("--balance", choices=["nodes", "messages"], default="nodes",
                    help="N > 1 destination shards: equal node blocks (C4's ids are randomly "
                         "permuted: messages within 2.6 %% at 8 ranks) or message-balanced ranges")
+    p.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
+                   help="N > 1 source-logits exchange: each rank receives only the rows its "
+                        "messages read (RCCL all-to-all; ~22 %% of the other ranks' nodes at "
+                        "C4 x8) or every node's (all-gather)")
     p.add_argument("--rehearse", action="store_true",
                    help="N > 1 ranks on however many GPUs are visible (rank -> GPU rank %% "
                         "count), gloo host-staged exchange: exercises the launcher and the "
@@ -132,7 +136,7 @@ def setup(dev, nodes, edges, F=166, gamma=2.1, dtype=torch.float32, rank=0, worl
 class Layer:
     """One GATConv layer-0 forward through the C ABI, split into timed stages."""
 
-    def __init__(self, s, dev, world):
+    def __init__(self, s, dev, world, exchange="halo"):
         from gfd import _lib
         self.s, self.dev, self.world = s, dev, world
         self.lib = _lib.load()
@@ -178,6 +182,13 @@ class Layer:
         if self.in_row:
             off, self.lds = s["s_row"]
             self.s_ptr = s["xbuf"].data_ptr() + 4 * off
+        # N > 1, halo exchange: the other ranks' rows this shard's messages read
+        # (plan built once here, by two all-to-alls of counts and row ids)
+        self.halo = None
+        if world > 1 and exchange == "halo":
+            from gfd import dist as gdist
+            lo, hi = int(g.rowptr[spec.dst_lo].item()), int(g.rowptr[spec.dst_hi].item())
+            self.halo = gdist.HaloPlan.create(g.col[lo:hi], spec)
 
     def logits_table(self):
         """[N, 16] s | t of the last step (tests): from the row slots or st."""
@@ -228,6 +239,17 @@ class Layer:
         # scale needs
         import torch.distributed as dist
         r = self.s["spec"].rank
+        if self.halo is not None:
+            # the rows this shard reads, straight into s_all (gfd_rows_copy pack,
+            # RCCL all-to-all, gfd_rows_copy scatter; gloo: host-staged)
+            self.halo.exchange(self.s_all)
+            if dist.get_backend() == "gloo":
+                xm = self.xmax.cpu()
+                dist.all_reduce(xm, op=dist.ReduceOp.MAX)
+                self.xmax.copy_(xm)
+            else:
+                dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
+            return
         if dist.get_backend() == "gloo":   # --rehearse: the same exchange, host-staged
             if not self.equal:
                 raise RuntimeError("--rehearse supports the node-balanced (equal-block) exchange")
@@ -323,7 +345,7 @@ def time_layer(layer, steps, warmup, world):
     return elapsed, stage_ms, mine
 
 
-def stage_bytes(s, plan, esz):
+def stage_bytes(s, plan, esz, halo=None):
     """Algorithmic bytes per stage (SURVEY.md §8d terms: a message gathers one
     x row + one int32 column index; a destination writes its fp32 out row and
     reads its rowptr entry; the weights once per kernel)."""
@@ -351,8 +373,9 @@ def stage_bytes(s, plan, esz):
     res = {
         "pack+logits": n_rows * (F * esz + 64) + W_b,
         "pack+logits+lone": n_rows * (F * esz + 64 + 4) + W_b + int(lone.sum().item()) * out_b,
-        # the all-gathered source logits land in HBM once: 32 B per node
-        "exchange": s["graph"].num_nodes * H * 4,
+        # the exchanged source logits land in HBM once: 32 B per node (all-gather)
+        # or per halo row received
+        "exchange": (halo.bytes_received(H) if halo is not None else s["graph"].num_nodes * H * 4),
         "hubs": hub_msgs * row_b + plan.num_chunks * 4 * (16 + 8 * ((F + 7) // 8 * 8)),
         "general": int(sdeg[gen & ~hubs_mask].sum().item()) * row_b +
                    int(gen.sum().item()) * out_b + W_b,
@@ -446,7 +469,7 @@ def measure(args, dev, rank, world, config):
     row_align = args.row_align or (128 if config == "c5" else 16)
     s = setup(dev, N, E, F, args.gamma, dtype, rank, world, row_align=row_align,
               balance=args.balance, s_in_row=not args.no_s_in_row)
-    layer = Layer(s, dev, world)
+    layer = Layer(s, dev, world, getattr(args, "exchange", "halo"))
     plan = layer.plan
     esz = s["xbuf"].element_size()
     log(f"[bench] {config} rank {rank}/{world}: N={N} E={E} messages={s['graph'].num_messages} "
@@ -463,7 +486,7 @@ def measure(args, dev, rank, world, config):
     flop_layer = 2 * N * F * H * C + M * H * (2 * C + 8)
     # per GPU: the layer's bytes and flops split over the ranks (dst sharding)
     t_roof = max(B_layer / (HBM_PEAK_GBPS * 1e9), flop_layer / (BF16_PEAK_TFLOPS * 1e12)) / world
-    sb, counts = stage_bytes(s, plan, esz)
+    sb, counts = stage_bytes(s, plan, esz, layer.halo)
     kernels = {}
     for name, ms in stage_ms.items():
         gbps = sb[name] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -472,7 +495,10 @@ def measure(args, dev, rank, world, config):
     dom = max((k for k in kernels if k != "exchange"), key=lambda k: kernels[k]["ms"])
     kname = {"pack+logits": "k_logits_s (+ pack)",
              "pack+logits+lone": "k_logits_lone (+ pack): logits + self-loop-only rows",
-             "exchange": "RCCL all-gather-v of the [N, 8] source logits + max|x| all-reduce",
+             "exchange": ("RCCL all-to-all of the halo rows of the [N, 8] source logits "
+                          "(gfd_rows_copy pack / scatter) + max|x| all-reduce"
+                          if layer.halo is not None else
+                          "RCCL all-gather-v of the [N, 8] source logits + max|x| all-reduce"),
              "hubs": "k_hub_partial + k_hub_fin",
              "general": "k_stream<general> (hub rows, 7+ messages)",
              "light": "k_stream<light> (2-6 messages)",
@@ -513,6 +539,9 @@ def measure(args, dev, rank, world, config):
         # ms_per_step is the max over ranks
         import torch.distributed as dist
         mine = {"rank": rank, "elapsed_s": rank_elapsed, "stage_ms": stage_ms,
+                "exchange": args.exchange,
+                "halo_rows": (int(layer.halo.recv_rows.numel()) if layer.halo is not None
+                              else None),
                 "dst": [s["spec"].dst_lo, s["spec"].dst_hi],
                 "messages": int(s["shard"].rowptr[-1].item() - s["shard"].rowptr[0].item()),
                 "device": torch.cuda.get_device_name(dev)}

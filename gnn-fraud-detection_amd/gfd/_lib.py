@@ -114,6 +114,7 @@ SIGNATURES = {
                                  P, P, P, P, P, P]),
     "gfd_atb_workspace_size": (c_sz, [c_i64, ct.c_int]),
     "gfd_atb": (c_i32, [P, c_i64, ct.c_int, P, c_i64, c_i64, P, P, P, c_sz, P]),
+    "gfd_rows_copy": (c_i32, [P, c_i64, P, P, c_i64, P, c_i64, ct.c_int, P]),
     "gfd_bn_workspace_size": (c_sz, []),
     "gfd_bn_relu_fwd": (c_i32, [P, P, c_i64, ct.c_int, P, P, c_f32, c_f32, P, P, ct.c_int, c_f32,
                                 c_u64, P, P, P, P, c_sz, P]),

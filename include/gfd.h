@@ -501,6 +501,18 @@ gfd_status gfd_bn_relu_bwd(const float* y, const float* grad_out, int64_t N, int
                            float* grad_y, float* grad_gamma, float* grad_beta, void* ws,
                            size_t ws_bytes, gfd_stream_t stream);
 
+/* -------------------------------------------------------------------------
+ * Sparse halo exchange between destination shards (gfd.dist.HaloPlan; the
+ * reference has no multi-GPU path -- this is the north star's "RCCL halo
+ * exchange" of per-node rows).  dst[dst_rows[i]] = src[src_rows[i]] for
+ * i < n, rows of ``cols`` fp32 values, row strides in floats; either index
+ * list may be NULL (identity).  Packs the rows a peer needs before the
+ * all-to-all and scatters the received ones to their node rows after it.
+ * ------------------------------------------------------------------------- */
+gfd_status gfd_rows_copy(const float* src, int64_t src_stride, const int32_t* src_rows,
+                         float* dst, int64_t dst_stride, const int32_t* dst_rows, int64_t n,
+                         int cols, gfd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

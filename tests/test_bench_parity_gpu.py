@@ -109,14 +109,18 @@ def test_c4_dst_shards(c4, world):
         del g._shards[k]
 
 
-@pytest.mark.parametrize("world,balance", [(2, "nodes"), (8, "nodes"), (8, "messages")])
-def test_bench_multi_rank_path(world, balance, monkeypatch):
+@pytest.mark.parametrize("world,balance,exchange", [
+    (2, "nodes", "allgather"), (8, "nodes", "allgather"), (8, "messages", "allgather"),
+    (2, "nodes", "halo"), (8, "nodes", "halo"), (8, "messages", "halo")])
+def test_bench_multi_rank_path(world, balance, exchange, monkeypatch):
     """bench.Layer's N > 1 path (the one the driver's scaling run times), rank by
-    rank on this GPU with the two collectives emulated from the whole-graph
-    run: the fused logits + lone pass over the rank's destinations, the
-    all-gather of the source logits (node balance: equal blocks, in place into
-    the padded table; message balance: uneven row views), the shard's tile
-    stage.  Every rank's rows equal the single-GPU layer's."""
+    rank on this GPU with the collectives emulated from the whole-graph run:
+    the fused logits + lone pass over the rank's destinations, the exchange of
+    the source logits -- all-gather (node balance: equal blocks, in place into
+    the padded table; message balance: uneven row views) or the halo
+    all-to-all (gfd_rows_copy packs the rows each peer reads, scatters the
+    received ones) -- and the shard's tile stage.  Every rank's rows equal the
+    single-GPU layer's."""
     import bench
     import torch.distributed as tdist
     from gfd import dist as gdist
@@ -155,20 +159,64 @@ def test_bench_multi_rank_path(world, balance, monkeypatch):
     def all_reduce(t, op=None, group=None):
         t.copy_(torch.maximum(t, xmax))
 
+    # halo: every rank's needs first (what its peers' all-to-alls deliver)
+    specs = [gdist.ShardSpec(g.rowptr, q, world, balance) for q in range(world)]
+    rp = g.rowptr.long()
+    needs = [gdist.halo_needs(g.col[int(rp[sp.dst_lo]):int(rp[sp.dst_hi])], sp) for sp in specs]
+    cur = {}
+
+    def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
+        assert exchange == "halo"
+        me = cur["rank"]
+        ids, cnt = needs[me]
+        offs = [0]
+        for c in cnt:
+            offs.append(offs[-1] + c)
+        if inp.dtype == torch.int64:      # plan: request counts -> what each peer wants
+            assert inp.tolist() == cnt
+            out.copy_(torch.tensor([needs[q][1][me] for q in range(world)], device=out.device))
+        elif inp.dtype == torch.int32:    # plan: requested ids -> the rows to send each peer
+            assert torch.equal(inp, ids) and input_split_sizes == cnt
+            parts = []
+            for q in range(world):
+                qo = sum(needs[q][1][:me])
+                parts.append(needs[q][0][qo:qo + needs[q][1][me]])
+            out.copy_(torch.cat(parts))
+        else:                             # a step: own rows out, the halo rows in
+            assert output_split_sizes == cnt
+            sent_rows = layer_ref["plan"].send_rows.long()
+            assert torch.equal(inp, st_full[sent_rows, :H]), f"rank {me}: sent rows"
+            out.copy_(st_full[ids.long(), :H])
+        return None
+
+    layer_ref = {}
     monkeypatch.setattr(tdist, "all_gather", all_gather)
     monkeypatch.setattr(tdist, "all_gather_into_tensor", all_gather_into_tensor)
     monkeypatch.setattr(tdist, "all_reduce", all_reduce)
+    monkeypatch.setattr(tdist, "all_to_all_single", all_to_all_single)
     monkeypatch.setattr(tdist, "get_backend", lambda group=None: "nccl")
     for r in range(world):
         sr = dict(s)
-        sr["spec"] = gdist.ShardSpec(g.rowptr, r, world, balance)
+        sr["spec"] = specs[r]
         sr["shard"] = g.shard(sr["spec"].dst_lo, sr["spec"].dst_hi)
-        layer = bench.Layer(sr, DEV, world)
+        cur["rank"] = r
+        layer = bench.Layer(sr, DEV, world, exchange)
+        if exchange == "halo":
+            layer_ref["plan"] = layer.halo
+            assert layer.halo.recv_counts == needs[r][1] and layer.halo.recv_counts[r] == 0
+            sent.append(r)
         layer.step()
         torch.cuda.synchronize()
         lo, hi = sr["spec"].dst_lo, sr["spec"].dst_hi
         # s | t of the own rows from the fused pass: bit-identical per-row arithmetic
-        assert torch.equal(layer.s_all[:g.num_nodes], st_full[:, :H]), f"rank {r}: s table"
+        if exchange == "halo":
+            rows = torch.cat([torch.arange(lo, hi, device=DEV), needs[r][0].long()])
+            assert torch.equal(layer.s_all[rows], st_full[rows, :H]), f"rank {r}: s rows"
+            # the halo is a fraction of the other ranks' nodes (~23 % at 8 ranks here)
+            frac = needs[r][0].numel() / (g.num_nodes - (hi - lo))
+            assert frac < (0.35 if world == 8 else 0.75), f"rank {r}: halo fraction {frac:.3f}"
+        else:
+            assert torch.equal(layer.s_all[:g.num_nodes], st_full[:, :H]), f"rank {r}: s table"
         assert torch.equal(layer.t_loc[:hi - lo], st_full[lo:hi, H:]), f"rank {r}: own t"
         assert sent[-1] == r
         assert_close(layer.out[:hi - lo], ref[lo:hi], atol=1e-5, rtol=1e-5,

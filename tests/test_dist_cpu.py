@@ -72,7 +72,10 @@ def _rank_main(rank, world, port, q):
                                            W, a_s, a_d, b)
         out = gdist.all_gather_v_rows(out_local, spec.dst_bounds)
         if rank == 0:
-            q.put((st, out, spec.dst_bounds, st_x, (spec.dst_lo, spec.dst_hi)))
+            # by value: a tensor would travel as a shared-memory handle that its
+            # sender's exit can invalidate before the parent unpickles it
+            q.put((st.numpy(), out.numpy(), spec.dst_bounds, st_x.numpy(),
+                   (spec.dst_lo, spec.dst_hi)))
     finally:
         dist.destroy_process_group()
 
@@ -86,6 +89,7 @@ def test_sharded_forward_matches_single_process(world):
     for p in procs:
         p.start()
     st, out, bounds, st_x, (d_lo, d_hi) = q.get(timeout=120)
+    st, out, st_x = torch.from_numpy(st), torch.from_numpy(out), torch.from_numpy(st_x)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -120,3 +124,62 @@ def test_node_bounds_cover():
         b = gdist.node_bounds(n, p)
         assert b[0] == 0 and b[-1] == n and len(b) == p + 1
         assert all(b[k] <= b[k + 1] for k in range(p))
+
+
+def _halo_main(rank, world, path, balance, q):
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
+    try:
+        ei, x, W, a_s, a_d, b = _problem()
+        rowptr, col = csr_cpu(ei, N)
+        spec = gdist.ShardSpec(rowptr, rank, world, balance)
+        shard_col = col[int(rowptr[spec.dst_lo]):int(rowptr[spec.dst_hi])]
+        plan = gdist.HaloPlan.create(shard_col, spec)
+        full = _logits(x, W, a_s, a_d)[:, :H].contiguous()
+        # a node-row table with only the own rows set (the fused logits pass's
+        # output); the halo exchange fills in exactly the rows the shard reads
+        table = torch.full((N, H), float("nan"))
+        table[spec.dst_lo:spec.dst_hi] = full[spec.dst_lo:spec.dst_hi]
+        plan.exchange(table)
+        need = torch.unique(shard_col.long())
+        ok_rows = bool(torch.equal(table[need], full[need]))
+        untouched = torch.ones(N, dtype=torch.bool)
+        untouched[need] = False
+        untouched[spec.dst_lo:spec.dst_hi] = False
+        stale = bool(torch.isnan(table[untouched]).all())
+        # the shard's aggregation over the halo-filled table matches the oracle
+        out_local = ref.gatconv_forward_at(x, rowptr, col, torch.arange(spec.dst_lo, spec.dst_hi),
+                                           W, a_s, a_d, b)
+        q.put((rank, ok_rows, stale, plan.recv_counts, plan.send_counts,
+               int(plan.recv_rows.numel()), out_local.numpy(), (spec.dst_lo, spec.dst_hi)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,balance", [(2, "nodes"), (3, "messages"), (4, "nodes")])
+def test_halo_exchange_delivers_exactly_the_rows_a_shard_reads(world, balance):
+    """gfd.dist.HaloPlan over gloo: the plan's all-to-alls of counts and ids,
+    then one exchange of the source-logit rows -- every row a shard's messages
+    read arrives bit-exact, no other row is written, rank q's sends to r are
+    r's requests from q, and the rows received are a fraction of the others'."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = _store_path()
+    procs = [ctx.Process(target=_halo_main, args=(r, world, path, balance, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_rows, stale, rc, sc, nrecv, _, (lo, hi) in res:
+        assert ok_rows, f"rank {rank}: halo rows"
+        assert stale, f"rank {rank}: wrote rows outside its halo"
+        assert rc[rank] == 0 and sc[rank] == 0 and sum(rc) == nrecv
+        for peer in range(world):
+            assert res[peer][4][rank] == rc[peer], "sends to r = r's requests"
+        assert nrecv < N - (hi - lo)
+    ei, x, W, a_s, a_d, b = _problem()
+    full = ref.gatconv_forward(x, ei, W, a_s, a_d, b, heads=H)
+    for rank, *_, out_local, (lo, hi) in res:
+        assert_close(torch.from_numpy(out_local), full[lo:hi], what=f"halo shard {rank} of {world}")

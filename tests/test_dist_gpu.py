@@ -126,3 +126,31 @@ def test_exchange_tables_are_read_and_written_in_place(balance):
         assert got.data_ptr() == nxt[lo:].data_ptr()
         assert torch.equal(got, want), f"rank {sp.rank}: strided tables differ"
     assert torch.all(nxt[:N, 64:] == 7.0), "the s columns of the next table were written"
+
+
+@pytest.mark.parametrize("cols,stride", [(8, 8), (8, 72), (72, 72), (5, 7)])
+def test_rows_copy_gather_scatter(cols, stride):
+    """gfd_rows_copy (the halo exchange's pack and scatter): gathered rows equal
+    torch indexing bit for bit, scattered rows land at their node rows and no
+    other row is written (16-B path: cols and strides multiples of 4; 4-B path
+    otherwise); strided column views as the hidden-layer table uses."""
+    from gfd import dist as gdist
+    g = torch.Generator(device="cuda").manual_seed(5)
+    n_rows, n = 10000, 3000
+    base = torch.randn((n_rows, stride), generator=g, device="cuda")
+    table = base[:, stride - cols:] if stride > cols else base
+    idx = torch.randperm(n_rows, generator=g, device="cuda")[:n].to(torch.int32)
+    buf = torch.empty((n, cols), device="cuda")
+    gdist.rows_copy(table, idx, buf, None)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, table[idx.long()])
+    dst_base = torch.full((n_rows, stride), float("nan"), device="cuda")
+    dst = dst_base[:, stride - cols:] if stride > cols else dst_base
+    gdist.rows_copy(buf, None, dst, idx)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[idx.long()], table[idx.long()])
+    untouched = torch.ones(n_rows, dtype=torch.bool, device="cuda")
+    untouched[idx.long()] = False
+    assert torch.isnan(dst_base[untouched]).all()
+    if stride > cols:
+        assert torch.isnan(dst_base[:, :stride - cols]).all()

@@ -115,7 +115,9 @@ def _rank_main(rank, world, port, q, balance="messages", chunks=4):
         with torch.no_grad():
             out = gdist.model_forward_sharded(m, x, (rowptr, col), spec, overlap_chunks=chunks)
         if rank == 0:
-            q.put(out)
+            # by value: a tensor would travel as a shared-memory handle that its
+            # sender's exit can invalidate before the parent unpickles it
+            q.put(out.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -136,7 +138,7 @@ def test_model_sharded_orchestration_gloo(world, balance, chunks):
              for r in range(world)]
     for p in procs:
         p.start()
-    out = q.get(timeout=180)
+    out = torch.from_numpy(q.get(timeout=180))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
