@@ -9,11 +9,14 @@ balanced by message count (prefix sum over in-degree).
 Layer 0 keeps ``x`` halo-resident (every rank holds the rows its in-edges
 reference; for a power-law graph that is nearly all of x).  Only the SOURCE
 logits s_j cross GPUs (``exchange_logits``): each rank computes ``[s | t]`` for
-its own destination block (whose t it is the only reader of) and all-gathers
+its own destination block (whose t it is the only reader of) and exchanges
 the s half (``[N, H]`` fp32: 32 B per node instead of the 664 B feature row --
 the "halo" of the north star).  The fused aggregate-project kernels then run on
-the local shard with no further communication.  Hidden layers all-gather the
+the local shard with no further communication.  Hidden layers exchange the
 previous layer's ``[N, 64]`` output rows together with the next layer's s.
+Every exchange is either the sparse halo exchange (``HaloPlan``: only the
+rows a shard's messages read, one RCCL all-to-all; the default of bench.py
+and model_forward_sharded) or an all-gather of every block (below).
 
 Layout (the split logits ABI, gfd_gat_aggregate_split): every exchanged table
 is laid out by node row, each rank's block where the all-gather puts it, so
@@ -341,13 +344,15 @@ def logits_rows(x: torch.Tensor, packed: torch.Tensor, lo: int, hi: int,
 
 def exchange_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
                     xmax: Optional[torch.Tensor] = None, group=None,
-                    logits_fn=None) -> LogitsTable:
+                    logits_fn=None, halo: Optional["HaloPlan"] = None) -> LogitsTable:
     """The logits a shard's aggregation reads: s of every node, t of the rank's
     destinations.  ONE logits pass per rank over its own destination block
     (the only rows whose t it reads), its s rows written into its block of an
     ``[rows, 8]`` exchange table, then one in-place all-gather of that table
     (``gather_blocks``: 32 B per node; half the bytes of gathering [s | t]).
-    ``logits_fn(lo, hi)`` -> [hi - lo, 16] replaces the HIP logits (tests)."""
+    ``logits_fn(lo, hi)`` -> [hi - lo, 16] replaces the HIP logits (tests).
+    ``halo``: exchange only the rows the shard reads (HaloPlan) instead of
+    all-gathering every block; the other rows of ``s`` are then not set."""
     H = 8
     N = x.size(0)
     if logits_fn is None:
@@ -359,7 +364,10 @@ def exchange_logits(x: torch.Tensor, packed: torch.Tensor, spec: ShardSpec,
     blk = logits_fn(spec.dst_lo, spec.dst_hi)
     s_tab = exchange_table(H, spec, blk.device)
     own_block(s_tab, spec).copy_(blk[:, :H])
-    gather_blocks(s_tab, spec, group)
+    if halo is not None:
+        halo.exchange(s_tab, group)
+    else:
+        gather_blocks(s_tab, spec, group)
     return LogitsTable(s_tab, blk[:, H:])
 
 
@@ -466,7 +474,8 @@ def shard_aggregate_ep(h: torch.Tensor, graph, st, packed: torch.Tensor,
 def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, residual: bool,
                           group=None, st=None, xmax: Optional[torch.Tensor] = None,
                           packed: Optional[torch.Tensor] = None,
-                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                          out: Optional[torch.Tensor] = None,
+                          halo: Optional["HaloPlan"] = None) -> torch.Tensor:
     """One layer body on this rank: source logits exchanged
     (``exchange_logits``) and max|x| reduced, the rank's destinations
     aggregated with BN / ReLU / residual in the store.  ``h`` is the layer
@@ -474,7 +483,8 @@ def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, res
     the gathered table's view).  ``st`` / ``xmax`` / ``packed``: the logits
     table, max |h| and the packed weights when the caller already has them
     (hidden layers: they come with the gathered rows).  ``out``: where the
-    output rows go (the rank's block of the next exchange table)."""
+    output rows go (the rank's block of the next exchange table).  ``halo``:
+    the source logits by the sparse exchange (exchange_logits)."""
     import torch.distributed as dist
     from .fused import bn_affine
     if packed is None:
@@ -482,7 +492,7 @@ def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, res
                               conv.att_dst.detach())
     if st is None:
         xmax = torch.zeros(1, dtype=torch.float32, device=h.device)
-        st = exchange_logits(h, packed, spec, xmax, group=group)
+        st = exchange_logits(h, packed, spec, xmax, group=group, halo=halo)
         if spec.world > 1:
             dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
     res = None
@@ -494,7 +504,8 @@ def layer_forward_sharded(conv, bn, h: torch.Tensor, graph, spec: ShardSpec, res
                               bn_affine(bn, h.device), True, res, out=out)
 
 
-def gather_hidden(table: torch.Tensor, next_conv, spec: ShardSpec, group=None):
+def gather_hidden(table: torch.Tensor, next_conv, spec: ShardSpec, group=None,
+                  halo: Optional["HaloPlan"] = None):
     """The exchange before a hidden layer, copy-free.  ``table`` is the
     ``[rows, 72]`` exchange table whose own block's columns 0..63 already hold
     this rank's output rows (the aggregation wrote them there).  The rank
@@ -502,7 +513,8 @@ def gather_hidden(table: torch.Tensor, next_conv, spec: ShardSpec, group=None):
     their s into columns 64..71 of its block, and ONE in-place all-gather
     fills every block; max |h| is reduced alongside.  Returns (h: [N, 64] view
     of the table, row stride 72; the LogitsTable: s = [N, 8] view of the
-    table, t = this rank's destinations; max |h|; the packed weights)."""
+    table, t = this rank's destinations; max |h|; the packed weights).
+    ``halo``: only the rows the shard reads are exchanged (72 floats each)."""
     import torch.distributed as dist
     H, C = 8, 64
     dev = table.device
@@ -514,7 +526,10 @@ def gather_hidden(table: torch.Tensor, next_conv, spec: ShardSpec, group=None):
     st_l = logits_rows(mine[:, :C], packed, 0, n_dst, xmax)
     if n_dst:
         mine[:, C:] = st_l[:, :H]
-    gather_blocks(table, spec, group)
+    if halo is not None:
+        halo.exchange(table, group)
+    else:
+        gather_blocks(table, spec, group)
     if spec.world > 1:
         dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
     n = spec.num_nodes
@@ -589,8 +604,16 @@ def layer_forward_gather_overlapped(conv, bn, h: torch.Tensor, graph, spec: Shar
     return table[:n, :C], LogitsTable(table[:n, C:], st_own[:, H:]), next_xmax, next_packed
 
 
+def shard_columns(graph, spec: ShardSpec) -> torch.Tensor:
+    """The CSR columns (global source ids) of the shard's messages; ``graph`` a
+    CSRGraph or a ``(rowptr, col)`` pair."""
+    rowptr, col = (graph.rowptr, graph.col) if hasattr(graph, "col") else graph
+    return col[int(rowptr[spec.dst_lo]):int(rowptr[spec.dst_hi])]
+
+
 def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=None,
-                          gather_output: bool = True, overlap_chunks: int = 4):
+                          gather_output: bool = True, overlap_chunks: int = 4,
+                          exchange: str = "halo"):
     """Destination-sharded eval forward of gfd.models.GAT / TemporalGNN (the
     reference's 2-3 layer stacks, gat.py:60-96, tgn.py:67-113) on this rank.
 
@@ -600,29 +623,40 @@ def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=
     72]`` exchange table, and ONE in-place collective (``gather_hidden``) moves
     them together with the next layer's source logits (computed by the row's
     owner): 2.9 GB in total at C4, no copies on either side of it.  The heads
-    (Linear, GRUCell + Linear) are row-local.  Returns the outputs of the
-    rank's destinations, or of all N nodes (gather_output).  Inference only."""
+    (Linear, GRUCell + Linear) are row-local.  ``exchange="halo"`` (default):
+    every exchange moves only the rows the shard's messages read (HaloPlan,
+    built once: ~22 % of the other ranks' rows at C4 over 8 ranks -- 0.6 GB
+    instead of 2.9 GB per hidden layer); ``"allgather"``: the in-place
+    all-gathers above, the hidden one in ``overlap_chunks`` pieces under the
+    aggregation (equal blocks).  Returns the outputs of the rank's
+    destinations, or of all N nodes (gather_output).  Inference only."""
     if model.training or torch.is_grad_enabled():
         raise RuntimeError("model_forward_sharded is inference-only: model.eval() and no_grad")
+    if exchange not in ("halo", "allgather"):
+        raise ValueError(f"exchange must be 'halo' or 'allgather', got {exchange!r}")
     h = x
     L = len(model.gat_layers)
     st = xmax = packed = None
+    halo = (HaloPlan.create(shard_columns(graph, spec), spec, group)
+            if exchange == "halo" and spec.world > 1 else None)
     for layer, conv in enumerate(model.gat_layers):
         bn = model.batch_norms[layer] if model.batch_norms is not None else None
         res = model.residual and h.size(-1) == model.hidden_channels
         if layer < L - 1 and spec.world > 1:
             table = exchange_table(HID, spec, x.device)
             nxt = model.gat_layers[layer + 1]
-            if spec.equal_blocks() and overlap_chunks > 1:   # collective under the compute
+            if halo is None and spec.equal_blocks() and overlap_chunks > 1:
+                # the all-gather under the compute
                 h, st, xmax, packed = layer_forward_gather_overlapped(
                     conv, bn, h, graph, spec, res, group, st, xmax, packed, table, nxt,
                     overlap_chunks)
             else:
                 layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed,
-                                      out=own_block(table, spec)[:, :64])
-                h, st, xmax, packed = gather_hidden(table, nxt, spec, group)
+                                      out=own_block(table, spec)[:, :64], halo=halo)
+                h, st, xmax, packed = gather_hidden(table, nxt, spec, group, halo=halo)
         else:
-            h = layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed)
+            h = layer_forward_sharded(conv, bn, h, graph, spec, res, group, st, xmax, packed,
+                                      halo=halo)
             st = xmax = packed = None
     if hasattr(model, "gru"):
         from .fused import gru_head

@@ -62,7 +62,10 @@ def _patch_oracle_stages(gdist, ei):
         # own destinations' t (checked against a recomputation)
         table = gdist._as_table(st, spec)
         full = logits_rows(h, packed, 0, h.size(0))
-        assert torch.allclose(table.s[:h.size(0)], full[:, :H], atol=1e-5, rtol=1e-5)
+        # the rows the shard reads (its sources; all rows after an all-gather)
+        rowptr, col = graph
+        rows = torch.unique(col[int(rowptr[spec.dst_lo]):int(rowptr[spec.dst_hi])].long())
+        assert torch.allclose(table.s[rows], full[rows, :H], atol=1e-5, rtol=1e-5)
         assert torch.allclose(table.t[:spec.dst_hi - spec.dst_lo], full[spec.dst_lo:spec.dst_hi, H:],
                               atol=1e-5, rtol=1e-5)
         rowptr, col = graph
@@ -97,7 +100,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, q, balance="messages", chunks=4):
+def _rank_main(rank, world, port, q, balance="messages", chunks=4, exchange="allgather"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "gnn-fraud-detection_amd")):
@@ -113,7 +116,8 @@ def _rank_main(rank, world, port, q, balance="messages", chunks=4):
         rowptr, col = csr_cpu(ei, N)
         spec = gdist.ShardSpec(rowptr, rank, world, balance)
         with torch.no_grad():
-            out = gdist.model_forward_sharded(m, x, (rowptr, col), spec, overlap_chunks=chunks)
+            out = gdist.model_forward_sharded(m, x, (rowptr, col), spec, overlap_chunks=chunks,
+                                              exchange=exchange)
         if rank == 0:
             # by value: a tensor would travel as a shared-memory handle that its
             # sender's exit can invalidate before the parent unpickles it
@@ -122,19 +126,23 @@ def _rank_main(rank, world, port, q, balance="messages", chunks=4):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,balance,chunks", [
-    (2, "messages", 4), (3, "messages", 4), (4, "messages", 4),
-    (3, "nodes", 1), (4, "nodes", 1),       # hidden exchange after the layer (gather_hidden)
-    (3, "nodes", 4), (4, "nodes", 3)])      # overlapped with the layer, in pieces
-def test_model_sharded_orchestration_gloo(world, balance, chunks):
+@pytest.mark.parametrize("world,balance,chunks,exchange", [
+    (2, "messages", 4, "allgather"), (3, "messages", 4, "allgather"),
+    (4, "messages", 4, "allgather"),
+    (3, "nodes", 1, "allgather"), (4, "nodes", 1, "allgather"),  # hidden exchange after the layer
+    (3, "nodes", 4, "allgather"), (4, "nodes", 3, "allgather"),  # overlapped, in pieces
+    (2, "nodes", 1, "halo"), (3, "messages", 1, "halo"), (4, "nodes", 1, "halo")])
+def test_model_sharded_orchestration_gloo(world, balance, chunks, exchange):
     """balance "nodes": equal blocks, every exchange one in-place all-gather
     into the layer's table -- or, before a hidden layer, ``chunks`` pieces
     all-gathered asynchronously under the aggregation of the next piece;
-    "messages": uneven blocks (gloo's padded path)."""
+    "messages": uneven blocks (gloo's padded path).  exchange "halo": every
+    exchange (layer 0's source logits, the hidden [h | s] rows) moves only
+    the rows each shard reads (HaloPlan all-to-alls)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _store_path()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, balance, chunks))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, balance, chunks, exchange))
              for r in range(world)]
     for p in procs:
         p.start()
