@@ -422,7 +422,7 @@ def shard_aggregate(x: torch.Tensor, graph, st, packed: torch.Tensor,
 def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torch.Tensor,
                      att_dst: torch.Tensor, bias: Optional[torch.Tensor], spec: ShardSpec,
                      negative_slope: float = 0.2, gather_output: bool = True,
-                     group=None) -> torch.Tensor:
+                     group=None, exchange: str = "halo") -> torch.Tensor:
     """Destination-sharded GATConv forward (eval) on this rank's GPU.
 
     ``x`` is halo-resident (all N rows on every rank, row stride may be
@@ -430,12 +430,17 @@ def gat_conv_sharded(x: torch.Tensor, graph, weight: torch.Tensor, att_src: torc
     (the own block's logits, one in-place all-gather of the SOURCE logits
     ``[N, 8]``) and max|x| reduced -> fused aggregate-project over the rank's
     destinations -> (optionally) all-gather of the ``[n_dst, 64]`` outputs.
+    ``exchange="halo"`` (default): the source logits by the sparse exchange
+    (only the rows the shard reads; the plan cached on the graph).
     """
     if x.stride(1) != 1:
         raise ValueError("x rows must be contiguous")
+    if exchange not in ("halo", "allgather"):
+        raise ValueError(f"exchange must be 'halo' or 'allgather', got {exchange!r}")
     packed = pack_weights(weight, att_src, att_dst)
     xmax = torch.zeros(1, dtype=torch.float32, device=x.device)
-    table = exchange_logits(x, packed, spec, xmax, group=group)
+    halo = halo_plan(graph, spec, group) if exchange == "halo" and spec.world > 1 else None
+    table = exchange_logits(x, packed, spec, xmax, group=group, halo=halo)
     if spec.world > 1:
         import torch.distributed as dist
         dist.all_reduce(xmax, op=dist.ReduceOp.MAX, group=group)
@@ -611,6 +616,22 @@ def shard_columns(graph, spec: ShardSpec) -> torch.Tensor:
     return col[int(rowptr[spec.dst_lo]):int(rowptr[spec.dst_hi])]
 
 
+def halo_plan(graph, spec: ShardSpec, group=None) -> "HaloPlan":
+    """The shard's HaloPlan, built once per (graph, destination range, world)
+    and cached on a CSRGraph (a ``(rowptr, col)`` pair: built every call)."""
+    key = (spec.dst_lo, spec.dst_hi, spec.world, spec.rank, id(group))
+    cache = getattr(graph, "_halo", None) if hasattr(graph, "_shards") else None
+    if cache is not None and key in cache:
+        return cache[key]
+    plan = HaloPlan.create(shard_columns(graph, spec), spec, group)
+    if hasattr(graph, "_shards"):
+        if cache is None:
+            cache = {}
+            graph._halo = cache
+        cache[key] = plan
+    return plan
+
+
 def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=None,
                           gather_output: bool = True, overlap_chunks: int = 4,
                           exchange: str = "halo"):
@@ -637,8 +658,7 @@ def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=
     h = x
     L = len(model.gat_layers)
     st = xmax = packed = None
-    halo = (HaloPlan.create(shard_columns(graph, spec), spec, group)
-            if exchange == "halo" and spec.world > 1 else None)
+    halo = halo_plan(graph, spec, group) if exchange == "halo" and spec.world > 1 else None
     for layer, conv in enumerate(model.gat_layers):
         bn = model.batch_norms[layer] if model.batch_norms is not None else None
         res = model.residual and h.size(-1) == model.hidden_channels

@@ -3,8 +3,8 @@ ONE GPU (the driver's 8-GPU scaling run is the real measurement; this is the
 single-GPU estimate of its compute part).
 
 For each rank r of a world of N: bench.setup with the rank's destination
-shard, bench.Layer(world = N) stepped with the two collectives emulated from
-the whole-graph run (the all-gathered s table and max |x| are copied in), and
+shard, bench.Layer(world = N) stepped with the collectives emulated from the
+whole-graph run (the exchanged s rows and max |x| are copied in), and
 the stage times from HIP events, median over --steps.  Prints one JSON line:
 per-rank stage ms, max over ranks of the compute stages, and the whole-graph
 single-GPU step for the ratio.
@@ -34,6 +34,7 @@ def main():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--nodes", type=int, default=10_000_000)
     p.add_argument("--edges", type=int, default=50_000_000)
+    p.add_argument("--exchange", choices=["halo", "allgather"], default="halo")
     a = p.parse_args()
     from gfd import dist as gdist
     dev = torch.device("cuda", 0)
@@ -56,16 +57,39 @@ def main():
     def all_reduce(t, op=None, group=None):
         t.copy_(torch.maximum(t, xmax))
 
+    # halo exchange: every rank's needs first; the all-to-all delivers the
+    # whole-graph run's rows (a device gather stands in for the xGMI transfer)
+    specs = [gdist.ShardSpec(g.rowptr, q, a.world, a.balance) for q in range(a.world)]
+    rp = g.rowptr.long()
+    needs = [gdist.halo_needs(g.col[int(rp[sp.dst_lo]):int(rp[sp.dst_hi])], sp) for sp in specs]
+    cur = {}
+
+    def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
+        me = cur["rank"]
+        ids, cnt = needs[me]
+        if inp.dtype == torch.int64:
+            out.copy_(torch.tensor([needs[q][1][me] for q in range(a.world)], device=out.device))
+        elif inp.dtype == torch.int32:
+            parts = []
+            for q in range(a.world):
+                qo = sum(needs[q][1][:me])
+                parts.append(needs[q][0][qo:qo + needs[q][1][me]])
+            out.copy_(torch.cat(parts))
+        else:
+            out.copy_(st_full[ids.long(), :8])
+
     tdist.all_gather_into_tensor = all_gather_into_tensor
     tdist.all_gather = all_gather
     tdist.all_reduce = all_reduce
+    tdist.all_to_all_single = all_to_all_single
     tdist.get_backend = lambda group=None: "nccl"
     ranks = []
     for r in range(a.world):
         sr = dict(s)
-        sr["spec"] = gdist.ShardSpec(g.rowptr, r, a.world, a.balance)
+        sr["spec"] = specs[r]
         sr["shard"] = g.shard(sr["spec"].dst_lo, sr["spec"].dst_hi)
-        layer = bench.Layer(sr, dev, a.world)
+        cur["rank"] = r
+        layer = bench.Layer(sr, dev, a.world, a.exchange)
         for _ in range(a.warmup):
             layer.step()
         nst = len(layer.stages)
@@ -80,6 +104,7 @@ def main():
         compute = sum(v for k, v in stage.items() if k != "exchange")
         sh = sr["shard"]
         ranks.append({"rank": r, "dst": [sr["spec"].dst_lo, sr["spec"].dst_hi],
+                      "halo_rows": int(needs[r][0].numel()) if a.exchange == "halo" else None,
                       "messages": int(sh.rowptr[-1].item() - sh.rowptr[0].item()),
                       "stage_ms": stage, "compute_ms": compute})
         del layer
@@ -88,11 +113,15 @@ def main():
         torch.cuda.empty_cache()
     worst = max(x["compute_ms"] for x in ranks)
     whole_step = el * 1e3 / a.steps
-    print(json.dumps({"world": a.world, "balance": a.balance, "whole_graph_ms": whole_step,
+    print(json.dumps({"world": a.world, "balance": a.balance, "exchange": a.exchange,
+                      "whole_graph_ms": whole_step,
                       "whole_stage_ms": whole_ms, "max_rank_compute_ms": worst,
                       "compute_speedup_bound": whole_step / worst,
-                      "note": "exchange (RCCL all-gather of N x 32 B + max all-reduce) not "
-                              "included: it needs the 8-GPU node", "ranks": ranks}))
+                      "note": "compute excludes the exchange stage; with --exchange halo that "
+                              "stage's time here is the on-GPU part (gfd_rows_copy pack and "
+                              "scatter, a device gather standing in for the all-to-all's "
+                              "transfer); the xGMI transfer needs the 8-GPU node",
+                      "ranks": ranks}))
 
 
 if __name__ == "__main__":
