@@ -18,17 +18,21 @@ namespace {
 
 constexpr int kRB = 256;
 
-// V floats per access (4: one 16-B load / store, 1: 4 B)
-template <int V>
+// V floats per access (4: one 16-B load / store, 1: 4 B); PER accesses per
+// row when known at compile time (2: the 8-float logits rows, 18: the 72-float
+// hidden rows), else the runtime ``per``.  Element counts below 2^31 (every
+// exchange here): 32-bit index arithmetic.
+template <int V, int PER>
 __global__ void __launch_bounds__(kRB) k_rows_copy(const float* __restrict__ src, int64_t lds,
                                                    const int32_t* __restrict__ sidx,
                                                    float* __restrict__ dst, int64_t ldd,
                                                    const int32_t* __restrict__ didx, int64_t n,
-                                                   int per) {
-  const int64_t total = n * per;
-  const int64_t step = int64_t(gridDim.x) * kRB;
-  for (int64_t i = int64_t(blockIdx.x) * kRB + threadIdx.x; i < total; i += step) {
-    const int64_t r = i / per;
+                                                   int per_rt) {
+  const uint32_t per = PER > 0 ? uint32_t(PER) : uint32_t(per_rt);
+  const uint32_t total = uint32_t(n) * per;
+  const uint32_t step = gridDim.x * kRB;
+  for (uint32_t i = blockIdx.x * kRB + threadIdx.x; i < total; i += step) {
+    const uint32_t r = i / per;
     const int c = int(i - r * per) * V;
     const int64_t rs = sidx ? int64_t(sidx[r]) : r;
     const int64_t rd = didx ? int64_t(didx[r]) : r;
@@ -57,14 +61,17 @@ gfd_status gfd_rows_copy(const float* src, int64_t src_stride, const int32_t* sr
                   reinterpret_cast<uintptr_t>(dst) % 16 == 0;
   const int per = v4 ? cols / 4 : cols;
   const int64_t total = n * per;
+  if (total >= (int64_t(1) << 31)) return GFD_ERR_UNSUPPORTED;
   int64_t grid = (total + kRB - 1) / kRB;
   if (grid > 8192) grid = 8192;  // grid-stride beyond 32 blocks per CU
-  if (v4)
-    k_rows_copy<4><<<int(grid), kRB, 0, stream>>>(src, src_stride, src_rows, dst, dst_stride,
-                                                  dst_rows, n, per);
-  else
-    k_rows_copy<1><<<int(grid), kRB, 0, stream>>>(src, src_stride, src_rows, dst, dst_stride,
-                                                  dst_rows, n, per);
+#define GFD_RC(V, PER)                                                                       \
+  k_rows_copy<V, PER><<<int(grid), kRB, 0, stream>>>(src, src_stride, src_rows, dst, dst_stride, \
+                                                     dst_rows, n, per)
+  if (v4 && per == 2) GFD_RC(4, 2);
+  else if (v4 && per == 18) GFD_RC(4, 18);
+  else if (v4) GFD_RC(4, 0);
+  else GFD_RC(1, 0);
+#undef GFD_RC
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }

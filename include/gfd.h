@@ -508,6 +508,7 @@ gfd_status gfd_bn_relu_bwd(const float* y, const float* grad_out, int64_t N, int
  * i < n, rows of ``cols`` fp32 values, row strides in floats; either index
  * list may be NULL (identity).  Packs the rows a peer needs before the
  * all-to-all and scatters the received ones to their node rows after it.
+ * GFD_ERR_UNSUPPORTED past 2^31 copied elements.
  * ------------------------------------------------------------------------- */
 gfd_status gfd_rows_copy(const float* src, int64_t src_stride, const int32_t* src_rows,
                          float* dst, int64_t dst_stride, const int32_t* dst_rows, int64_t n,

@@ -63,6 +63,7 @@ def main():
     rp = g.rowptr.long()
     needs = [gdist.halo_needs(g.col[int(rp[sp.dst_lo]):int(rp[sp.dst_hi])], sp) for sp in specs]
     cur = {}
+    st_src = st_full[:, :8].contiguous()
 
     def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
         me = cur["rank"]
@@ -75,8 +76,8 @@ def main():
                 qo = sum(needs[q][1][:me])
                 parts.append(needs[q][0][qo:qo + needs[q][1][me]])
             out.copy_(torch.cat(parts))
-        else:
-            out.copy_(st_full[ids.long(), :8])
+        else:   # the transfer's stand-in: one more row copy out of the full table
+            gdist.rows_copy(st_src, ids, out, None)
 
     tdist.all_gather_into_tensor = all_gather_into_tensor
     tdist.all_gather = all_gather
