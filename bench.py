@@ -62,9 +62,12 @@ def parse(argv=None):
                    help="byte alignment of x rows (16: fp32 pitch 176 with the s slot; 128: "
                         "whole cache lines).  Default: 16 for C4, 128 for C5 (bf16 rows: "
                         "measured -1.6 ms at C5, +0.1 ms at C4)")
-    p.add_argument("--balance", choices=["nodes", "messages"], default="nodes",
-                   help="N > 1 destination shards: equal node blocks (C4's ids are randomly "
-                        "permuted: messages within 2.6 %% at 8 ranks) or message-balanced ranges")
+    p.add_argument("--balance", choices=["nodes", "messages", "cost"], default="cost",
+                   help="N > 1 destination shards: ranges balanced by the modelled "
+                        "per-destination stage time (default; C4 x8 rank by rank: slowest "
+                        "rank 2.03 ms against 2.06 for equal node blocks), equal node blocks "
+                        "(C4's ids are randomly permuted: messages within 2.6 %% at 8 ranks) "
+                        "or message-balanced ranges")
     p.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
                    help="N > 1 source-logits exchange: each rank receives only the rows its "
                         "messages read (RCCL all-to-all; ~22 %% of the other ranks' nodes at "

@@ -56,6 +56,48 @@ def edge_balanced_bounds(rowptr: torch.Tensor, parts: int) -> List[int]:
     return bounds
 
 
+# Per-destination time model of the forward's stages on one MI355X (ns; C4
+# round-4 stage times over their classes: logits pass 2.1 ms / 10M rows,
+# light 6.1 ms / 6.2M rows, general 2.9 ms / 15.4M messages, hubs 2.3 ms /
+# 21.3M messages plus a light-like projection row): what ``balance="cost"``
+# equalises across ranks.
+COST_ROW_NS, COST_LIGHT_NS, COST_GEN_MSG_NS, COST_HUB_MSG_NS, COST_HUB_ROW_NS = \
+    0.21, 0.98, 0.19, 0.108, 1.0
+
+
+def destination_costs(rowptr: torch.Tensor) -> torch.Tensor:
+    """Modelled forward time of every destination (float64, ns) from its
+    in-degree (self loop included): lone (1 message) -- the logits pass only;
+    light (2..6); general (7..128, per message); hubs (> 128, per message plus
+    the projection row).  Thresholds as the plan's (gfd_common.h, graph.py)."""
+    from .graph import HUB_THRESHOLD
+    deg = (rowptr[1:] - rowptr[:-1]).to(torch.float64)
+    cost = torch.full_like(deg, COST_ROW_NS)
+    cost += torch.where((deg >= 2) & (deg <= 6), COST_LIGHT_NS, 0.0)
+    cost += torch.where((deg > 6) & (deg <= HUB_THRESHOLD), COST_GEN_MSG_NS * deg, 0.0)
+    cost += torch.where(deg > HUB_THRESHOLD, COST_HUB_MSG_NS * deg + COST_HUB_ROW_NS, 0.0)
+    return cost
+
+
+def cost_balanced_bounds(rowptr: torch.Tensor, parts: int) -> List[int]:
+    """Destination boundaries with ~equal modelled time per part
+    (``destination_costs``): the node blocks of a randomly permuted power-law
+    graph are equal in rows but not in hub messages (C4 at 8 ranks: the hub
+    stage 0.36-0.50 ms across equal node blocks)."""
+    n = rowptr.numel() - 1
+    if parts <= 1 or n == 0:
+        return [0, n]
+    pre = torch.cumsum(destination_costs(rowptr), 0)
+    total = float(pre[-1].item())
+    targets = torch.tensor([total * k / parts for k in range(1, parts)], dtype=pre.dtype,
+                           device=pre.device)
+    cuts = torch.searchsorted(pre, targets).add_(1).clamp_(0, n).tolist()
+    bounds = [0] + [int(c) for c in cuts] + [n]
+    for k in range(1, len(bounds)):
+        bounds[k] = max(bounds[k], bounds[k - 1])
+    return bounds
+
+
 def node_bounds(n: int, parts: int) -> List[int]:
     """Equal contiguous node blocks, padded so every block has ceil(n/parts) rows."""
     per = (n + parts - 1) // parts
@@ -85,7 +127,9 @@ class ShardSpec:
 
     ``dst_lo:dst_hi`` -- the destinations (and so the CSR messages) this rank
     owns; their attention logits are this rank's share of the exchange.
-    ``balance="messages"``: ranges balanced by message count (prefix sum over
+    ``balance="cost"``: ranges balanced by the modelled forward time of their
+    destinations (``cost_balanced_bounds``; for the halo exchange, which takes
+    any ranges).  ``balance="messages"``: ranges balanced by message count (prefix sum over
     in-degree); ``"nodes"``: equal node blocks of ``per = ceil(N / world)``
     rows (last one shorter) -- on a graph with randomly permuted ids (C4) the
     message counts then differ by ~2.6 % at 8 ranks, the destination counts
@@ -98,11 +142,12 @@ class ShardSpec:
     def __init__(self, rowptr: torch.Tensor, rank: int, world: int, balance: str = "messages"):
         n = rowptr.numel() - 1
         self.rank, self.world, self.num_nodes = rank, world, n
-        if balance not in ("messages", "nodes"):
-            raise ValueError(f"balance must be 'messages' or 'nodes', got {balance!r}")
+        if balance not in ("messages", "nodes", "cost"):
+            raise ValueError(f"balance must be 'messages', 'nodes' or 'cost', got {balance!r}")
         self.balance = balance
         self.node_bounds = node_bounds(n, world)
         self.dst_bounds = (edge_balanced_bounds(rowptr, world) if balance == "messages"
+                           else cost_balanced_bounds(rowptr, world) if balance == "cost"
                            else list(self.node_bounds))
         self.per = max(max(self.dst_bounds[r + 1] - self.dst_bounds[r] for r in range(world)), 1)
         self.dst_lo, self.dst_hi = self.dst_bounds[rank], self.dst_bounds[rank + 1]

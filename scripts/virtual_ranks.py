@@ -29,7 +29,7 @@ import bench  # noqa: E402
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--world", type=int, default=8)
-    p.add_argument("--balance", choices=["nodes", "messages"], default="nodes")
+    p.add_argument("--balance", choices=["nodes", "messages", "cost"], default="nodes")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--nodes", type=int, default=10_000_000)

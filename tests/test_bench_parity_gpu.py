@@ -111,7 +111,7 @@ def test_c4_dst_shards(c4, world):
 
 @pytest.mark.parametrize("world,balance,exchange", [
     (2, "nodes", "allgather"), (8, "nodes", "allgather"), (8, "messages", "allgather"),
-    (2, "nodes", "halo"), (8, "nodes", "halo"), (8, "messages", "halo")])
+    (2, "nodes", "halo"), (8, "nodes", "halo"), (8, "messages", "halo"), (8, "cost", "halo")])
 def test_bench_multi_rank_path(world, balance, exchange, monkeypatch):
     """bench.Layer's N > 1 path (the one the driver's scaling run times), rank by
     rank on this GPU with the collectives emulated from the whole-graph run:

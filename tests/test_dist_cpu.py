@@ -155,7 +155,8 @@ def _halo_main(rank, world, path, balance, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,balance", [(2, "nodes"), (3, "messages"), (4, "nodes")])
+@pytest.mark.parametrize("world,balance", [(2, "nodes"), (3, "messages"), (4, "nodes"),
+                                           (3, "cost")])
 def test_halo_exchange_delivers_exactly_the_rows_a_shard_reads(world, balance):
     """gfd.dist.HaloPlan over gloo: the plan's all-to-alls of counts and ids,
     then one exchange of the source-logit rows -- every row a shard's messages
@@ -183,3 +184,22 @@ def test_halo_exchange_delivers_exactly_the_rows_a_shard_reads(world, balance):
     full = ref.gatconv_forward(x, ei, W, a_s, a_d, b, heads=H)
     for rank, *_, out_local, (lo, hi) in res:
         assert_close(torch.from_numpy(out_local), full[lo:hi], what=f"halo shard {rank} of {world}")
+
+
+def test_cost_balanced_bounds_equalise_the_modelled_time():
+    """balance="cost": contiguous, monotone ranges covering every destination,
+    each within one destination's cost of the mean modelled time -- and a
+    graph with a few heavy hubs is split unevenly in nodes to do it."""
+    from gfd import synth
+    N = 50_000
+    ei = torch.from_numpy(synth.power_law(N, 250_000, seed=3))
+    rowptr, _ = csr_cpu(ei, N)
+    cost = gdist.destination_costs(rowptr)
+    for world in (2, 3, 8):
+        b = gdist.ShardSpec(rowptr, 0, world, "cost").dst_bounds
+        assert b[0] == 0 and b[-1] == N and all(b[k] <= b[k + 1] for k in range(world))
+        parts = [float(cost[b[r]:b[r + 1]].sum()) for r in range(world)]
+        mean = sum(parts) / world
+        assert max(abs(p - mean) for p in parts) <= float(cost.max()) + 1e-9
+    sizes = {b[r + 1] - b[r] for r in range(8)}
+    assert len(sizes) > 1
