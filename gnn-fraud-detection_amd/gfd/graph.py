@@ -29,7 +29,11 @@ import torch
 from . import _lib
 
 HUB_THRESHOLD = int(os.environ.get("GFD_HUB_THRESHOLD", "128"))
-HUB_CHUNK = int(os.environ.get("GFD_HUB_CHUNK", "256"))
+# messages per hub chunk (one wave each): 384 against 256 -- C4 hubs stage
+# 2.28 -> 2.25 ms, C5 23.0 -> 22.6 ms, and at 8 destination shards the slowest
+# rank 2.03 -> 1.95 ms (fewer partials to merge, whole waves per shard);
+# 128 / 64 are slower everywhere (profiles/r4e_hub_chunk.txt)
+HUB_CHUNK = int(os.environ.get("GFD_HUB_CHUNK", "384"))
 # source hubs of the backward's CSC pass (k_bwd_src chunks)
 SRC_HUB_THRESHOLD = 512
 SRC_HUB_CHUNK = 512
