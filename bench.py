@@ -68,10 +68,12 @@ def parse(argv=None):
                         "rank 2.03 ms against 2.06 for equal node blocks), equal node blocks "
                         "(C4's ids are randomly permuted: messages within 2.6 %% at 8 ranks) "
                         "or message-balanced ranges")
-    p.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
+    p.add_argument("--exchange", choices=["halo", "halo1", "allgather"], default="halo",
                    help="N > 1 source-logits exchange: each rank receives only the rows its "
                         "messages read (RCCL all-to-all; ~22 %% of the other ranks' nodes at "
-                        "C4 x8) or every node's (all-gather)")
+                        "C4 x8), in two phases whose first runs under the second half of the "
+                        "logits pass (halo) or in one after it (halo1); or every node's "
+                        "(allgather)")
     p.add_argument("--rehearse", action="store_true",
                    help="N > 1 ranks on however many GPUs are visible (rank -> GPU rank %% "
                         "count), gloo host-staged exchange: exercises the launcher and the "
@@ -188,10 +190,14 @@ class Layer:
         # N > 1, halo exchange: the other ranks' rows this shard's messages read
         # (plan built once here, by two all-to-alls of counts and row ids)
         self.halo = None
-        if world > 1 and exchange == "halo":
+        self.halo_parts = None   # "halo": the two row-range phases of the exchange
+        self.pending = []
+        if world > 1 and exchange in ("halo", "halo1"):
             from gfd import dist as gdist
             lo, hi = int(g.rowptr[spec.dst_lo].item()), int(g.rowptr[spec.dst_hi].item())
             self.halo = gdist.HaloPlan.create(g.col[lo:hi], spec)
+            if exchange == "halo":
+                self.halo_parts = self.halo.split(spec, 2)
 
     def logits_table(self):
         """[N, 16] s | t of the last step (tests): from the row slots or st."""
@@ -229,12 +235,25 @@ class Layer:
                       self.packed.data_ptr(), H, C, self.st.data_ptr(), self.xmax.data_ptr(),
                       self.stream)
             self.s_all.copy_(self.st[:, :H])
-        if n > 0:
-            _lib.call("gfd_gat_logits_lone_split", x[spec.dst_lo:].data_ptr(), self.xdt, n, F,
-                      s["ldx"], self.packed.data_ptr(), H, C, s["shard"].rowptr.data_ptr(),
-                      s["bias"].data_ptr(), 0.2, self.s_all[spec.dst_lo:].data_ptr(), H,
-                      self.t_loc.data_ptr(), H, self.xmax.data_ptr(), self.out.data_ptr(), C,
-                      None, self.stream)
+
+        def logits(a, b):   # own destinations a..b (local rows)
+            if b > a:
+                lo = spec.dst_lo + a
+                _lib.call("gfd_gat_logits_lone_split", x[lo:].data_ptr(), self.xdt, b - a, F,
+                          s["ldx"], self.packed.data_ptr(), H, C,
+                          s["shard"].rowptr[a:].data_ptr(), s["bias"].data_ptr(), 0.2,
+                          self.s_all[lo:].data_ptr(), H, self.t_loc[a:].data_ptr(), H,
+                          self.xmax.data_ptr(), self.out[a:].data_ptr(), C, None, self.stream)
+        if self.halo_parts is not None:
+            # phase k of the halo exchange leaves as soon as its rows' logits are
+            # written; phase 0's collective runs under the second half's pass
+            self.pending = []
+            cut = [n * k // len(self.halo_parts) for k in range(len(self.halo_parts) + 1)]
+            for k, part in enumerate(self.halo_parts):
+                logits(cut[k], cut[k + 1])
+                self.pending.append(part.exchange_async(self.s_all))
+            return
+        logits(0, n)
 
     def exchange(self):
         # ONE all-gather-v of the [N, 8] source logits (RCCL; uneven blocks land
@@ -244,8 +263,14 @@ class Layer:
         r = self.s["spec"].rank
         if self.halo is not None:
             # the rows this shard reads, straight into s_all (gfd_rows_copy pack,
-            # RCCL all-to-all, gfd_rows_copy scatter; gloo: host-staged)
-            self.halo.exchange(self.s_all)
+            # RCCL all-to-all, gfd_rows_copy scatter; gloo: host-staged); the
+            # phased form was issued by pack_and_logits and is completed here
+            if self.halo_parts is not None:
+                for finish in self.pending:
+                    finish()
+                self.pending = []
+            else:
+                self.halo.exchange(self.s_all)
             if dist.get_backend() == "gloo":
                 xm = self.xmax.cpu()
                 dist.all_reduce(xm, op=dist.ReduceOp.MAX)
@@ -499,7 +524,10 @@ def measure(args, dev, rank, world, config):
     kname = {"pack+logits": "k_logits_s (+ pack)",
              "pack+logits+lone": "k_logits_lone (+ pack): logits + self-loop-only rows",
              "exchange": ("RCCL all-to-all of the halo rows of the [N, 8] source logits "
-                          "(gfd_rows_copy pack / scatter) + max|x| all-reduce"
+                          "(gfd_rows_copy pack / scatter) + max|x| all-reduce" +
+                          (" -- two row-range phases, the first issued under the second "
+                           "half of the logits pass (its wait and scatter timed here)"
+                           if layer.halo_parts is not None else "")
                           if layer.halo is not None else
                           "RCCL all-gather-v of the [N, 8] source logits + max|x| all-reduce"),
              "hubs": "k_hub_partial + k_hub_fin",

@@ -302,6 +302,38 @@ class HaloPlan:
     def bytes_received(self, cols: int, esz: int = 4) -> int:
         return int(self.recv_rows.numel()) * cols * esz
 
+    def split(self, spec: ShardSpec, parts: int = 2) -> List["HaloPlan"]:
+        """The same exchange in ``parts`` phases by row range: phase k moves the
+        rows in the k-th of ``parts`` sub-ranges ``lo + (hi - lo) * k // parts``
+        of each owner's destination block, so an owner can send phase k as soon
+        as its logits pass has written that sub-range (the rest of the pass runs
+        under the collective).  Every row of the plan is in exactly one phase."""
+        b = spec.dst_bounds
+
+        def cuts(q):
+            lo, hi = b[q], b[q + 1]
+            return [lo + (hi - lo) * k // parts for k in range(parts + 1)]
+
+        def split_groups(rows, counts, cut_of):
+            out_rows = [[] for _ in range(parts)]
+            out_counts = [[0] * len(counts) for _ in range(parts)]
+            off = 0
+            for g, c in enumerate(counts):
+                seg = rows[off:off + c]
+                off += c
+                cs = torch.tensor(cut_of(g)[1:-1], dtype=seg.dtype, device=seg.device)
+                pos = torch.searchsorted(seg, cs).tolist() if c else [0] * (parts - 1)
+                edges = [0] + [int(v) for v in pos] + [c]
+                for k in range(parts):
+                    out_rows[k].append(seg[edges[k]:edges[k + 1]])
+                    out_counts[k][g] = edges[k + 1] - edges[k]
+            return [torch.cat(r) if r else rows[:0] for r in out_rows], out_counts
+
+        rr, rc = split_groups(self.recv_rows, self.recv_counts, cuts)          # owner q's cuts
+        sr, sc = split_groups(self.send_rows, self.send_counts,
+                              lambda g: cuts(spec.rank))                       # own cuts
+        return [HaloPlan(rr[k], rc[k], sr[k], sc[k]) for k in range(parts)]
+
     def _buf(self, key, rows, like: torch.Tensor) -> torch.Tensor:
         shape = (max(rows, 1), like.size(1))
         b = self._bufs.get(key)
@@ -314,20 +346,38 @@ class HaloPlan:
         """``table`` (``[rows >= N, cols]`` fp32 by node row, unit column stride,
         any row stride): the rank's own rows are valid; afterwards so are its
         halo rows.  Rows neither own nor halo are not written."""
+        self.exchange_async(table, group)()
+
+    def exchange_async(self, table: torch.Tensor, group=None):
+        """``exchange`` split at the collective: packs the own rows and issues
+        the all-to-all (RCCL: asynchronously, on its own stream, ordered after
+        the pack); returns ``finish()``, which makes the current stream wait
+        for it and scatters the received rows.  gloo (CPU tests, host-staged
+        rehearsals): synchronous."""
         import torch.distributed as dist
         ns, nr = int(self.send_rows.numel()), int(self.recv_rows.numel())
         send = self._buf("send", ns, table)
         recv = self._buf("recv", nr, table)
         rows_copy(table, self.send_rows, send, None)
+        work = None
         if table.is_cuda and dist.get_backend(group) == "gloo":   # rehearsal: host-staged
             rc = torch.empty((max(nr, 1), table.size(1)), dtype=table.dtype)
             dist.all_to_all_single(rc[:nr], send[:ns].cpu(), output_split_sizes=self.recv_counts,
                                    input_split_sizes=self.send_counts, group=group)
             recv[:nr].copy_(rc[:nr])
+        elif table.is_cuda:
+            work = dist.all_to_all_single(recv[:nr], send[:ns], output_split_sizes=self.recv_counts,
+                                          input_split_sizes=self.send_counts, group=group,
+                                          async_op=True)
         else:
             dist.all_to_all_single(recv[:nr], send[:ns], output_split_sizes=self.recv_counts,
                                    input_split_sizes=self.send_counts, group=group)
-        rows_copy(recv, None, table, self.recv_rows)
+
+        def finish():
+            if work is not None:
+                work.wait()
+            rows_copy(recv, None, table, self.recv_rows)
+        return finish
 
 
 def all_gather_v_rows(local: torch.Tensor, bounds: List[int], group=None) -> torch.Tensor:

@@ -34,7 +34,7 @@ def main():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--nodes", type=int, default=10_000_000)
     p.add_argument("--edges", type=int, default=50_000_000)
-    p.add_argument("--exchange", choices=["halo", "allgather"], default="halo")
+    p.add_argument("--exchange", choices=["halo", "halo1", "allgather"], default="halo")
     a = p.parse_args()
     from gfd import dist as gdist
     dev = torch.device("cuda", 0)
@@ -65,7 +65,8 @@ def main():
     cur = {}
     st_src = st_full[:, :8].contiguous()
 
-    def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
+    def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None,
+                          async_op=False):
         me = cur["rank"]
         ids, cnt = needs[me]
         if inp.dtype == torch.int64:
@@ -77,7 +78,15 @@ def main():
                 parts.append(needs[q][0][qo:qo + needs[q][1][me]])
             out.copy_(torch.cat(parts))
         else:   # the transfer's stand-in: one more row copy out of the full table
-            gdist.rows_copy(st_src, ids, out, None)
+            plans = cur["plans"]
+            pl = plans[cur["phase"] % len(plans)]
+            cur["phase"] += 1
+            gdist.rows_copy(st_src, pl.recv_rows, out, None)
+
+        class _Done:
+            def wait(self):
+                return True
+        return _Done() if async_op else None
 
     tdist.all_gather_into_tensor = all_gather_into_tensor
     tdist.all_gather = all_gather
@@ -89,8 +98,9 @@ def main():
         sr = dict(s)
         sr["spec"] = specs[r]
         sr["shard"] = g.shard(sr["spec"].dst_lo, sr["spec"].dst_hi)
-        cur["rank"] = r
+        cur["rank"], cur["phase"] = r, 0
         layer = bench.Layer(sr, dev, a.world, a.exchange)
+        cur["plans"] = (layer.halo_parts or [layer.halo]) if layer.halo is not None else None
         for _ in range(a.warmup):
             layer.step()
         nst = len(layer.stages)
@@ -105,7 +115,7 @@ def main():
         compute = sum(v for k, v in stage.items() if k != "exchange")
         sh = sr["shard"]
         ranks.append({"rank": r, "dst": [sr["spec"].dst_lo, sr["spec"].dst_hi],
-                      "halo_rows": int(needs[r][0].numel()) if a.exchange == "halo" else None,
+                      "halo_rows": int(needs[r][0].numel()) if a.exchange != "allgather" else None,
                       "messages": int(sh.rowptr[-1].item() - sh.rowptr[0].item()),
                       "stage_ms": stage, "compute_ms": compute})
         del layer

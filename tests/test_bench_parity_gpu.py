@@ -111,7 +111,8 @@ def test_c4_dst_shards(c4, world):
 
 @pytest.mark.parametrize("world,balance,exchange", [
     (2, "nodes", "allgather"), (8, "nodes", "allgather"), (8, "messages", "allgather"),
-    (2, "nodes", "halo"), (8, "nodes", "halo"), (8, "messages", "halo"), (8, "cost", "halo")])
+    (2, "nodes", "halo"), (8, "nodes", "halo"), (8, "messages", "halo"), (8, "cost", "halo"),
+    (8, "cost", "halo1")])
 def test_bench_multi_rank_path(world, balance, exchange, monkeypatch):
     """bench.Layer's N > 1 path (the one the driver's scaling run times), rank by
     rank on this GPU with the collectives emulated from the whole-graph run:
@@ -165,8 +166,9 @@ def test_bench_multi_rank_path(world, balance, exchange, monkeypatch):
     needs = [gdist.halo_needs(g.col[int(rp[sp.dst_lo]):int(rp[sp.dst_hi])], sp) for sp in specs]
     cur = {}
 
-    def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
-        assert exchange == "halo"
+    def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None,
+                          async_op=False):
+        assert exchange in ("halo", "halo1")
         me = cur["rank"]
         ids, cnt = needs[me]
         offs = [0]
@@ -183,11 +185,18 @@ def test_bench_multi_rank_path(world, balance, exchange, monkeypatch):
                 parts.append(needs[q][0][qo:qo + needs[q][1][me]])
             out.copy_(torch.cat(parts))
         else:                             # a step: own rows out, the halo rows in
-            assert output_split_sizes == cnt
-            sent_rows = layer_ref["plan"].send_rows.long()
-            assert torch.equal(inp, st_full[sent_rows, :H]), f"rank {me}: sent rows"
-            out.copy_(st_full[ids.long(), :H])
-        return None
+            plans = layer_ref["plans"]
+            k = cur["phase"] % len(plans)  # the phases are issued in order
+            cur["phase"] += 1
+            pl = plans[k]
+            assert output_split_sizes == pl.recv_counts and input_split_sizes == pl.send_counts
+            assert torch.equal(inp, st_full[pl.send_rows.long(), :H]), f"rank {me}: sent rows"
+            out.copy_(st_full[pl.recv_rows.long(), :H])
+
+        class _Done:
+            def wait(self):
+                return True
+        return _Done() if async_op else None
 
     layer_ref = {}
     monkeypatch.setattr(tdist, "all_gather", all_gather)
@@ -199,17 +208,22 @@ def test_bench_multi_rank_path(world, balance, exchange, monkeypatch):
         sr = dict(s)
         sr["spec"] = specs[r]
         sr["shard"] = g.shard(sr["spec"].dst_lo, sr["spec"].dst_hi)
-        cur["rank"] = r
+        cur["rank"], cur["phase"] = r, 0
         layer = bench.Layer(sr, DEV, world, exchange)
-        if exchange == "halo":
-            layer_ref["plan"] = layer.halo
+        if exchange in ("halo", "halo1"):
+            layer_ref["plans"] = layer.halo_parts or [layer.halo]
             assert layer.halo.recv_counts == needs[r][1] and layer.halo.recv_counts[r] == 0
+            if layer.halo_parts:   # the phases partition the plan
+                assert sum(int(p.recv_rows.numel()) for p in layer.halo_parts) == \
+                    layer.halo.recv_rows.numel()
+                assert torch.equal(torch.sort(torch.cat([p.recv_rows for p in layer.halo_parts]))[0],
+                                   layer.halo.recv_rows)
             sent.append(r)
         layer.step()
         torch.cuda.synchronize()
         lo, hi = sr["spec"].dst_lo, sr["spec"].dst_hi
         # s | t of the own rows from the fused pass: bit-identical per-row arithmetic
-        if exchange == "halo":
+        if exchange in ("halo", "halo1"):
             rows = torch.cat([torch.arange(lo, hi, device=DEV), needs[r][0].long()])
             assert torch.equal(layer.s_all[rows], st_full[rows, :H]), f"rank {r}: s rows"
             # the halo is a fraction of the other ranks' nodes (~23 % at 8 ranks here)

@@ -142,6 +142,12 @@ def _halo_main(rank, world, path, balance, q):
         plan.exchange(table)
         need = torch.unique(shard_col.long())
         ok_rows = bool(torch.equal(table[need], full[need]))
+        # the same exchange in two row-range phases (bench's overlapped form)
+        table2 = torch.full((N, H), float("nan"))
+        table2[spec.dst_lo:spec.dst_hi] = full[spec.dst_lo:spec.dst_hi]
+        for part in plan.split(spec, 2):
+            part.exchange_async(table2)()
+        ok_rows = ok_rows and bool(torch.equal(table2[need], full[need]))
         untouched = torch.ones(N, dtype=torch.bool)
         untouched[need] = False
         untouched[spec.dst_lo:spec.dst_hi] = False
