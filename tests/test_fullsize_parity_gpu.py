@@ -90,7 +90,7 @@ def test_c5_full_size_sampled_parity(c5):
     layer = bench.Layer(s, DEV, 1)
     light_b, lone_b = layer.plan.classes()
     assert 0 < light_b < lone_b < s["graph"].num_nodes
-    assert layer.plan.num_chunks > 1_000_000                 # the C5 hub-chunk regime
+    assert layer.plan.num_chunks > 500_000                   # the C5 hub-chunk regime (384-message chunks)
     layer.step()
     torch.cuda.synchronize()
     out = layer.out
