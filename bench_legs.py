@@ -150,47 +150,68 @@ def c2_gat3_train_step(dev, steps=20, warmup=3, cpu_runs=3):
 def _c2_parity(m, d, mask, yl, dev):
     """One fwd + BCE + bwd step of the leg's weights with dropout 0 (the
     counter-based masks are not torch's RNG stream) on the device and in the
-    oracle: max |logits error| and the largest gradient error relative to its
-    tensor's max (tests/test_fullsize_models_gpu.py asserts the same bounds)."""
+    oracle run in float64, per tensor: max |error|, max |ref| and the error
+    over the bound tests/test_fullsize_models_gpu.py asserts (2e-4 max|ref| +
+    1e-5).  The reference is fp64 because the fp32 oracle's own rounding
+    breaches that bound at these weights (2.05x on gat_layers.1.lin_src.weight
+    against fp64, where the device is at 0.000x: profiles/r5a_c2_breach_diag.txt);
+    the fp32 oracle's error is reported beside it for context."""
     from gfd.models import GAT
     from oracle import GATRef
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     g = GAT(165, 64, 1, num_layers=3, dropout=0.0)
     g.load_state_dict(sd, strict=True)
     g = g.to(dev).train()
-    r = GATRef(165, 64, 1, num_layers=3, dropout=0.0).train()
-    r.load_state_dict(sd, strict=True)
     x = d["x"].clone().requires_grad_(True)
     crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0], device=dev))
     lg = g(x, d["edge_index"])
     crit(lg[mask].squeeze(1), yl).backward()
-    xr = d["x"].cpu().requires_grad_(True)
-    lr = r(xr, d["edge_index"].cpu())
-    torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0]))(
-        lr[mask.cpu()].squeeze(1), yl.cpu()).backward()
-    rp = dict(r.named_parameters())
-    rel = [(x.grad.cpu() - xr.grad).abs().max().item() / xr.grad.abs().max().item()]
-    zero, tol = [], [0.0]
-    for name, p in g.named_parameters():
-        if p.grad is None or name.endswith("lin_dst.weight"):
-            continue
-        err = (p.grad.cpu() - rp[name].grad).abs().max().item()
-        den = rp[name].grad.abs().max().item()
-        tol.append(err / (2e-4 * den + 1e-5))   # the test's bound (tests/_util.py)
+    got = {"x": x.grad.cpu().double()}
+    got.update({n: p.grad.cpu().double() for n, p in g.named_parameters()
+                if p.grad is not None and not n.endswith("lin_dst.weight")})
+
+    def oracle(dtype):
+        r = GATRef(165, 64, 1, num_layers=3, dropout=0.0).train()
+        r.load_state_dict(sd, strict=True)
+        r = r.to(dtype)
+        xr = d["x"].cpu().to(dtype).requires_grad_(True)
+        lr = r(xr, d["edge_index"].cpu())
+        torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0], dtype=dtype))(
+            lr[mask.cpu()].squeeze(1), yl.cpu().to(dtype)).backward()
+        out = {"x": xr.grad.double()}
+        out.update({n: p.grad.double() for n, p in r.named_parameters() if p.grad is not None})
+        return out, lr.detach().double()
+
+    r64, l64 = oracle(torch.float64)
+    r32, _ = oracle(torch.float32)
+    per, zero = [], []
+    worst, worst32, worst_rel = 0.0, 0.0, 0.0
+    for name, a in got.items():
+        ref = r64[name]
+        den = ref.abs().max().item()
+        bound = 2e-4 * den + 1e-5                 # the test's bound (tests/_util.py)
+        err = (a - ref).abs().max().item()
+        err32 = (r32[name] - ref).abs().max().item()
+        per.append({"tensor": name, "max_abs_err": err, "max_abs_ref": den,
+                    "err_over_tolerance": err / bound, "oracle_f32_err_over_tolerance": err32 / bound})
         if den < 1e-6:   # analytically zero: a GATConv bias under train-mode BatchNorm
             zero.append(name)
-        else:
-            rel.append(err / den)
-    return {"max_abs_err_vs_oracle": (lg.detach().cpu() - lr.detach()).abs().max().item(),
-            "max_grad_rel_err_vs_oracle": max(rel),
-            "max_grad_err_over_tolerance": max(tol),
-            "zero_grad_params": zero,
-            "parity_note": "dropout 0 step, same weights: logits max abs error; gradients: max "
-                           "|error| / max |oracle grad| over x and every parameter whose "
-                           "gradient is not analytically zero (zero_grad_params: biases "
-                           "feeding train-mode BatchNorm, where both sides are rounding "
-                           "noise); max_grad_err_over_tolerance <= 1: every gradient within "
-                           "2e-4 max|ref| + 1e-5"}
+            continue
+        worst, worst32 = max(worst, err / bound), max(worst32, err32 / bound)
+        worst_rel = max(worst_rel, err / den)
+    return {"max_abs_err_vs_oracle": (lg.detach().cpu().double() - l64).abs().max().item(),
+            "max_grad_rel_err_vs_oracle": worst_rel,
+            "max_grad_err_over_tolerance": worst,
+            "oracle_f32_max_grad_err_over_tolerance": worst32,
+            "zero_grad_params": zero, "grad_parity": per,
+            "parity_note": "dropout 0 step, same weights, against the oracle in float64: logits "
+                           "max abs error; per tensor (grad_parity) max |error|, max |ref| and "
+                           "error / (2e-4 max|ref| + 1e-5), the bound of "
+                           "tests/test_fullsize_models_gpu.py; max_grad_* over every tensor "
+                           "whose gradient is not analytically zero (zero_grad_params: GATConv "
+                           "biases feeding train-mode BatchNorm, both sides rounding noise, "
+                           "still listed in grad_parity); <= 1 is within bound. "
+                           "oracle_f32_*: the fp32 oracle's own error against fp64"}
 
 
 def c3_tgn_49_steps(dev, steps=20, warmup=3, cpu_runs=3):

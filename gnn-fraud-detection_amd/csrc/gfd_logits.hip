@@ -10,7 +10,7 @@
 // ~2^-21 relative) for the rows whose in-degree is 1 saves the lone kernel's
 // second read of those rows.
 //
-// k_logits_lone: 8-wave blocks, two per CU, grid-stride over 16-row tiles.
+// k_logits_lone: one 16-wave block per CU, grid-stride over 16-row tiles.
 //   * lane (r = l & 15, g = l >> 4) loads features 16 s + 4 g .. +3 of row r
 //     for every fp32 k-step s (fp32), or 32 t + 8 g .. +7 for every f16
 //     k-step t (bf16) -- 16-B loads, all issued before the first MFMA;
@@ -24,6 +24,14 @@
 //     fragments (12 more MFMAs per k-step);
 //   * out rows (and, in training, the softmax stats: max = leaky(s_i + t_i),
 //     denominator 1) are written for lone rows only.
+//   * stores: the MFMA results (lane = column, 4 rows per lane) are turned
+//     row-major through a per-wave LDS scratch tile, so every lane writes 16 B
+//     of one row -- the 16 rows' s | t in ONE store instruction (rows' 32-B s
+//     slot and 32-B t row), a lone row's 256-B output in 16 lanes, both as
+//     non-temporal stores (C4 pass 2.15 -> 1.98 ms).  The writes (1.35 GB at
+//     C4) are what holds the pass above its read-only speed: without the s / t
+//     stores it takes 1.72 ms, without them, the lone outputs and with
+//     contiguous loads 1.18 (profiles/r5b_logits_ablation.txt).
 #include "gfd_fwd.h"
 
 using namespace gfd;
@@ -31,13 +39,21 @@ using namespace gfd::fwd;
 
 namespace {
 
-constexpr int kLLWaves = 8;  // 512-thread blocks, two per CU (LDS 60 KB each)
+constexpr int kLLWaves = 16;  // 1024-thread blocks, one per CU (LDS 128.5 KB)
+constexpr int kTP = 68;        // scratch tile row pitch (floats): conflict-free column writes
 constexpr int kLKS = 12;     // fp32 k-steps of 16 features (F <= 192)
 constexpr int kLKB = 6;      // f16 k-steps of 32 features
 
 // KS fp32 k-steps held per row (11: F <= 176, the f16 k-step 5 pairs step 10
 // with zeros; 12: F <= 192).  HEAD: the model head folded into the lone rows'
 // store (its own instance: the plain one stays inside 128 VGPRs, no spill)
+// Order this wave's scratch-tile accesses as written (the hardware runs one
+// wave's LDS operations in order; this keeps the compiler from moving them)
+__device__ __forceinline__ void lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <typename XT, int KS, bool HEAD>
 __global__ void __launch_bounds__(kLLWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_logits_lone(
@@ -48,9 +64,16 @@ k_logits_lone(
     float* __restrict__ sl, int lds, float* __restrict__ tl, int ldt, float* __restrict__ xmax,
     float* __restrict__ out,
     float* __restrict__ stats, Epi ep) {
-  __shared__ uint4 WB[2][kLKB][4][64];  // permuted Wbar hi / lo fragments, zero past KB
-  __shared__ uint4 UP[2][kLKB][64];     // permuted [U | V] hi / lo fragments, zero past KB
-  __shared__ float BH[2][C];            // bias and (HEAD) head weights for the launch
+  extern __shared__ __attribute__((aligned(16))) char lsm[];
+  // permuted Wbar hi / lo fragments [2][kLKB][4][64], zero past KB
+  uint4 (*WB)[kLKB][4][64] = reinterpret_cast<uint4 (*)[kLKB][4][64]>(lsm);
+  // permuted [U | V] hi / lo fragments [2][kLKB][64], zero past KB
+  uint4 (*UP)[kLKB][64] = reinterpret_cast<uint4 (*)[kLKB][64]>(lsm + sizeof(uint4) * 2 * kLKB * 4 * 64);
+  // bias and (HEAD) head weights for the launch [2][C]
+  float (*BH)[C] = reinterpret_cast<float (*)[C]>(lsm + sizeof(uint4) * 2 * kLKB * 5 * 64);
+  // this wave's row-major scratch tile [16][kTP]
+  float* T = reinterpret_cast<float*>(lsm + sizeof(uint4) * 2 * kLKB * 5 * 64 + sizeof(float) * 2 * C) +
+             __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (16 * kTP);
   const int KB = (F + 31) / 32;
   const int kst = (F + 15) / 16;  // fp32 k-steps incl. the ragged tail
   const int ksf = F / 16;         // fp32 k-steps fully inside the row
@@ -69,8 +92,13 @@ k_logits_lone(
     BH[1][i] = HEAD ? ep.hw[i] : 0.f;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int rl = lane & 15, g = lane >> 4;
+  const int lane0 = threadIdx.x & 63;
+  // 16-B row stores when every row start of the table is 16-B aligned (kernel-uniform)
+  const int st_vec = __builtin_amdgcn_readfirstlane(
+      (reinterpret_cast<uintptr_t>(sl) % 16 == 0) && lds % 4 == 0 &&
+      (reinterpret_cast<uintptr_t>(tl) % 16 == 0) && ldt % 4 == 0);
+  const int out_vec = __builtin_amdgcn_readfirstlane(
+      (reinterpret_cast<uintptr_t>(out) % 16 == 0) && ep.ldo % 4 == 0);
   const float wbu = hdr->wb_unscale;
   const float uvu = hdr->uv_unscale;
   float am = 0.f;  // max |x| over the values this lane loaded
@@ -78,6 +106,7 @@ k_logits_lone(
   const int64_t nwave = int64_t(gridDim.x) * kLLWaves;
   const int64_t tiles = (rows + 15) / 16;
   for (int64_t t = wave; t < tiles; t += nwave) {
+    int lane = lane0, rl = lane & 15, g = lane >> 4;
     const int64_t row = t * 16 + rl;
     const bool rin = row < rows;
     // fp32: lane group g holds features 16 s + 4 g .. +3 of fp32 k-step s (the
@@ -112,6 +141,10 @@ k_logits_lone(
       }
     } else {
       const typename XT::T* xr = x + (rin ? row : rows - 1) * ldx + 4 * g;
+#ifdef GFD_AB_LOGITS_COAL
+      // ablation only (wrong results): every load one contiguous 1 KB of the tile
+      const typename XT::T* xc = x + (t * 16 < rows - 16 ? t * 16 : rows - 16) * ldx + 4 * lane;
+#endif
 #pragma unroll
       for (int s = 0; s < kLKS; ++s) {
         if (s >= KS) {
@@ -119,7 +152,11 @@ k_logits_lone(
           continue;
         }
         if (s < ksf) {
+#ifdef GFD_AB_LOGITS_COAL
+          a[s] = load4<XT>(xc + 256 * s);
+#else
           a[s] = load4<XT>(xr + 16 * s);
+#endif
         } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
 #pragma unroll
           for (int u = 0; u < 4; ++u) a[s][u] = 16 * s + 4 * g + u < F ? xcvt(xr[16 * s + u]) : 0.f;
@@ -133,7 +170,11 @@ k_logits_lone(
     }
     const bool lone = rin && rowptr[row + 1] - rowptr[row] == 1;
     am = fmaxf(am, rm);  // clamped tail rows repeat row rows - 1: harmless for a max
+#ifdef GFD_AB_LOGITS_NOLONE
+    const bool any_lone = __ballot(lone && rowptr[0] < 0) != 0;  // ablation only: no lone outputs
+#else
     const bool any_lone = __ballot(lone) != 0;  // wave-uniform
+#endif
     const int er = scale_exp(max_xor16_32(rm));  // lanes r, r + 16, r + 32, r + 48
     const float rs = ldexpf(1.0f, er);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -178,7 +219,12 @@ k_logits_lone(
       }
     }
     // acc / o[ct] element q of lane l: row 4 g + q, column rl (16 ct + rl);
-    // the row's unscale comes from a lane holding that row
+    // the row's unscale comes from a lane holding that row.  (Lane-derived
+    // addresses below are recomputed per tile from an opaque lane id rather
+    // than hoisted out of the loop and pinned in VGPRs.)
+    lane = opaque(lane0);
+    rl = lane & 15;
+    g = lane >> 4;
     const float ers = ldexpf(1.0f, -er);
     float sv[4];
 #pragma unroll
@@ -186,25 +232,56 @@ k_logits_lone(
       const int src = 4 * g + q;
       const float eq = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers)));
       sv[q] = acc[q] * (eq * uvu);
-      const int64_t orow = t * 16 + src;
-      // s | t columns of the row (sl / tl: separate tables, any strides)
-      if (orow < rows)
-        (rl < H ? sl + uint64_t(uint32_t(orow)) * uint32_t(lds)
-                : tl + uint64_t(uint32_t(orow)) * uint32_t(ldt) - H)[rl] = sv[q];
+      T[src * kTP + rl] = sv[q];
+    }
+    lds_order();  // the wave's LDS ops run in order: no wait needed
+    {  // row r = lane / 4, quarter lane % 4 (s 0..3, s 4..7, t 0..3, t 4..7)
+      const int r = lane >> 2, qd = lane & 3;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(T + r * kTP + 4 * qd);
+      const int64_t orow = t * 16 + r;
+#ifdef GFD_AB_LOGITS_NOST
+      if (orow < 0) {  // ablation only: no s / t stores
+#else
+      if (orow < rows) {
+#endif
+        // two stores under complementary lane masks keep both table bases scalar
+        auto put = [&](float* dst) {
+          if (st_vec) {
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dst[i] = v[i];
+          }
+        };
+        if (qd < 2) put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd);
+        else put(tl + uint64_t(uint32_t(orow)) * uint32_t(ldt) + 4 * (qd - 2));
+      }
+    }
+    const int lone_i = lone ? 1 : 0;
+    if (__builtin_expect(stats != nullptr, 0) && any_lone) {  // training (no dropout) only
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int src = 4 * g + q;
+        const int lq = __builtin_amdgcn_ds_bpermute(src << 2, lone_i);
+        // the row's t logits (columns 8..15) next to its s logits (0..7)
+        const float tq = dpp_mov<0x128>(sv[q]);  // row_ror:8 within the 16-lane row
+        if (lq && rl < H) {
+          const int64_t orow = t * 16 + src;
+          stats[orow * 16 + rl] = leaky(sv[q] + tq, slope);
+          stats[orow * 16 + H + rl] = 1.0f;
+        }
+      }
     }
     if (!any_lone) continue;
-    const int lone_i = lone ? 1 : 0;
+    if constexpr (HEAD) {  // model head: one dot per row instead of the row
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int src = 4 * g + q;  // a lane holding row src's flag and scale
-      const int lq = __builtin_amdgcn_ds_bpermute(src << 2, lone_i);
-      const float uq =
-          __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers))) * wbu;
-      // the row's t logits (columns 8..15) next to its s logits (0..7)
-      const float tq = dpp_mov<0x128>(sv[q]);  // row_ror:8 within the 16-lane row
-      if (lq) {  // uniform over the 16 lanes of the row (lane group g)
-        const int64_t orow = t * 16 + src;
-        if constexpr (HEAD) {  // model head: one dot per row instead of the row
+      for (int q = 0; q < 4; ++q) {
+        const int src = 4 * g + q;  // a lane holding row src's flag and scale
+        const int lq = __builtin_amdgcn_ds_bpermute(src << 2, lone_i);
+        const float uq =
+            __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers))) * wbu;
+        if (lq) {  // uniform over the 16 lanes of the row (lane group g)
+          const int64_t orow = t * 16 + src;
           float d = 0.f;
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
@@ -212,17 +289,44 @@ k_logits_lone(
                      BH[1][ct * 16 + rl], d);
           d = row16_sum(d);
           if (rl == 0) ep.hout[orow] = d + (ep.hb ? ep.hb[0] : 0.f);
-        } else {
-          float* orp = out + uint64_t(uint32_t(orow)) * uint32_t(ep.ldo) + rl;
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct)
-            orp[ct * 16] =
-                epi_store_value(o[ct][q] * uq, BH[0][ct * 16 + rl], ct * 16 + rl,
-                                orow, ep);
         }
-        if (__builtin_expect(stats != nullptr, 0) && rl < H) {  // training (no dropout) only
-          stats[orow * 16 + rl] = leaky(sv[q] + tq, slope);
-          stats[orow * 16 + H + rl] = 1.0f;
+      }
+    } else {
+      // out rows through the scratch tile: lane (g, rl) writes rows 4 g + q,
+      // columns 16 ct + rl; then 16 lanes x 16 B per row
+      lds_order();
+      int lq[4];
+      float uq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int src = 4 * g + q;
+        lq[q] = __builtin_amdgcn_ds_bpermute(src << 2, lone_i);
+        uq[q] = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(ers))) * wbu;
+      }
+      // the epilogue (its residual read) only for lone rows: other rows' slots are not stored
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int n = ct * 16 + rl;
+        const float bn = BH[0][n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          T[(4 * g + q) * kTP + n] =
+              lq[q] ? epi_store_value(o[ct][q] * uq[q], bn, n, t * 16 + 4 * g + q, ep) : 0.f;
+      }
+      lds_order();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * i + g, ch = rl;  // row r, 16-B chunk ch of its 64 columns
+        const int lr = __builtin_amdgcn_ds_bpermute(r << 2, lone_i);  // lane r holds row r's flag
+        const f32x4 v = *reinterpret_cast<const f32x4*>(T + r * kTP + 4 * ch);
+        if (lr) {
+          float* orp = out + uint64_t(uint32_t(t * 16 + r)) * uint32_t(ep.ldo) + 4 * ch;
+          if (out_vec) {
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(orp));
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) orp[k] = v[k];
+          }
         }
       }
     }
@@ -230,7 +334,7 @@ k_logits_lone(
   if (xmax) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
-    if (lane == 0) atomic_max_nonneg(xmax, am);
+    if (lane0 == 0) atomic_max_nonneg(xmax, am);
   }
 }
 
@@ -241,12 +345,15 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
                     float* stats, const Epi& ep, hipStream_t stream) {
   const int64_t tiles = (rows + 15) / 16;
   int64_t nb = (tiles + kLLWaves - 1) / kLLWaves;
-  const int64_t cap = int64_t(cu_count()) * 2;  // resident blocks; grid-stride beyond
+  const int64_t cap = int64_t(cu_count());  // resident blocks; grid-stride beyond
   if (nb > cap) nb = cap;
   auto kern = ep.hout ? (F <= 176 ? &k_logits_lone<XT, 11, true> : &k_logits_lone<XT, 12, true>)
                       : (F <= 176 ? &k_logits_lone<XT, 11, false> : &k_logits_lone<XT, 12, false>);
+  const size_t smem = sizeof(uint4) * 2 * kLKB * 5 * 64 + sizeof(float) * 2 * C +
+                      sizeof(float) * kLLWaves * 16 * kTP;
+  if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
   const bool plain = XT::kBytes == 2;  // bf16: plain-order fragments (16-B loads)
-  kern<<<int(nb), kLLWaves * 64, 0, stream>>>(
+  kern<<<int(nb), kLLWaves * 64, smem, stream>>>(
       static_cast<const typename XT::T*>(x), rows, F, ldx,
       reinterpret_cast<const PackHeader*>(packed + L.hdr_off),
       reinterpret_cast<const uint4*>(packed + (plain ? L.ush_off : L.uph_off)),
