@@ -343,6 +343,35 @@ __device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[NR][K
   }
 }
 
+// fma_k with the message weights from LDS: ab[8 k + h] = p of message k, head
+// h (the wave wrote its 64 lanes' p there); two broadcast 16-B reads per
+// message give the four head pairs as VGPR pairs -- 2 LDS reads instead of 8
+// v_readlane per message.
+template <int KF, int K, int NR>
+__device__ __forceinline__ void fma_k_lds(f32x2 (&z)[4][KF], const float (&xr)[NR][KF],
+                                          const float* __restrict__ ab) {
+  static_assert(K <= NR, "rows past the prefetched ones");
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(ab + 8 * k);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(ab + 8 * k + 4);
+    const f32x2 p2[4] = {f32x2{a0.x, a0.y}, f32x2{a0.z, a0.w}, f32x2{a1.x, a1.y},
+                         f32x2{a1.z, a1.w}};
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq)
+        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
+    // (keeps the compiler from hoisting every read of the slot: the register
+    // budget has no room for them)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // One destination segment (or hub chunk) on one wave, single pass with an
 // online softmax.  Logit lane layout: lane = 8 k + h (message k of a batch of
 // 8, head h); aggregation lane layout: lane <-> feature f = lane + 64 q.

@@ -48,6 +48,14 @@ using namespace gfd::fwd;
 namespace {
 
 constexpr int kSWaves = 8;
+// Light slots: message weights broadcast through LDS (fma_k_lds: 2 broadcast
+// reads per message instead of 8 v_readlane; the light kernel's VALU count
+// -25 %) -- measured neutral (C4 light 6.34-6.61 vs 6.36-6.51 ms across three
+// box pairs, C5 34.3 vs 33.7 ms: profiles/r5c_light_ablation.txt), so off by
+// default: the kernel is not bound by its VALU count
+#ifndef GFD_LIGHT_ALDS
+#define GFD_LIGHT_ALDS 0
+#endif
 #ifndef GFD_LIGHT_AP
 #define GFD_LIGHT_AP 1
 #endif
@@ -105,6 +113,7 @@ struct SlotRows {  // a slot's first (and, for light slots, only) batch in fligh
   float th;        // t_i of head lane & 7
   float sj;        // s_j of the lane's message (lane >> 3)
   int cj;          // general: source of message 8 + lane (0 past the end)
+  int n;           // messages of the slot (wave-uniform; set with the logits)
   float xv[NRW][KF];  // x rows of messages 0 .. NRW - 1 (lane <-> feature)
 };
 
@@ -138,6 +147,7 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW
     const int e1 = __builtin_amdgcn_readlane(p.v, 2);
     const int hw = __builtin_amdgcn_readlane(p.v, 3);
     const int jm = __builtin_amdgcn_ds_bpermute((8 + (lane >> 3)) << 2, p.v);  // message lane >> 3
+    q.n = e1 - e0;
     q.th = lrow(t, row, ldt)[h];
     q.sj = lrow(s, jm, lds)[h];
     if constexpr (!LIGHT) {
@@ -155,8 +165,7 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW
     // padding sources repeat the last one) fetch nothing and read zeros
     constexpr int k = PART - 1;
     const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
-    const int n = __builtin_amdgcn_readlane(p.v, 2) - __builtin_amdgcn_readlane(p.v, 1);
-    row_regs<XT, KF>(xrow<XT>(x, jk, ldx), F, lane, k < n, q.xv[k]);
+    row_regs<XT, KF>(xrow<XT>(x, jk, ldx), F, lane, k < q.n, q.xv[k]);
   }
 }
 
@@ -174,6 +183,19 @@ __device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[k
   else fma_k<KF, kLightMax>(z, xv, p);
 }
 
+// light_fma with the weights from the wave's LDS buffer (fma_k_lds)
+template <int KF>
+__device__ __forceinline__ void light_fma_lds(f32x2 (&z)[4][KF],
+                                              const float (&xv)[kLightMax][KF],
+                                              const float* __restrict__ ab, int kmax) {
+  if (kmax <= 2) fma_k_lds<KF, 2>(z, xv, ab);
+  else if (kmax == 3) fma_k_lds<KF, 3>(z, xv, ab);
+  else if (kLightMax == 4 || kmax == 4) fma_k_lds<KF, 4>(z, xv, ab);
+  else if (kLightMax == 5 || kmax == 5) fma_k_lds<KF, (kLightMax >= 5 ? 5 : 4)>(z, xv, ab);
+  else if (kLightMax == 6 || kmax == 6) fma_k_lds<KF, (kLightMax >= 6 ? 6 : 4)>(z, xv, ab);
+  else fma_k_lds<KF, kLightMax>(z, xv, ab);
+}
+
 // A slot with at most kLightMax messages (all rows prefetched), not a hub
 // (with dropout also the self-loop-only slots: their heads are masked one by
 // one, so the head-mean shortcut of k_lone does not apply): straight-line
@@ -185,13 +207,27 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLight
                                          float* __restrict__ stats,
                                          _Float16* __restrict__ zh, _Float16* __restrict__ zl,
                                          float* __restrict__ rsc, int* __restrict__ rid, int r,
-                                         int erg, int lane) {
+                                         int erg, float* __restrict__ ab, int lane) {
   if (d.x < 0) {  // past the last destination
     if (lane == 0) rid[r] = -1;
     return;
   }
   const int kk = lane >> 3;
   const int n = d.z - d.y;
+#ifdef GFD_AB_LIGHT_NOAGG  // ablation only (wrong results): rows consumed, no softmax / FMA / Z write
+  {
+    float f = q.sj + q.th;
+#pragma unroll
+    for (int k = 0; k < kLightMax; ++k)
+#pragma unroll
+      for (int qq = 0; qq < KF; ++qq) f += q.xv[k][qq];
+    if (lane == 0) {
+      rsc[r] = f;
+      rid[r] = d.x;
+    }
+    return;
+  }
+#endif
   const float v = leaky01(q.sj + q.th, slope);
   const float m = max_xor8_16_32(kk < n ? v : -INFINITY);
   const float p = kk < n ? __expf(v - m) : 0.f;
@@ -216,10 +252,20 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLight
     // one scale for every row: fold 1 / (sum + eps) and 2^erg into the
     // weights, so z comes out normalised and scaled and only needs the split
     const float ps = pd * (inv * ldexpf(1.0f, erg));
+#if GFD_LIGHT_ALDS
+    ab[lane] = ps;  // this wave's own buffer: its LDS operations run in order
+    light_fma_lds<KF>(z, q.xv, ab, kmax);
+#else
     light_fma<KF>(z, q.xv, ps, kmax);
+#endif
     split_zrow<KF>(z, hi, lo);
   } else {
+#if GFD_LIGHT_ALDS
+    ab[lane] = pd;
+    light_fma_lds<KF>(z, q.xv, ab, kmax);
+#else
     light_fma<KF>(z, q.xv, pd, kmax);
+#endif
     er = pack_zrow<KF>(z, inv, erg, hi, lo);
   }
   write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
@@ -468,10 +514,14 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     if constexpr (LIGHT) {
       const int4 da = uni4(rg[r0].d), db = uni4(rg[r1].d);
       const int kmax = max(da.z - da.y, db.z - db.y);  // wave-uniform
+      // message-weight buffers: the kh = 1 partials region of this tile's
+      // parity, free between barrier 1 and the next MFMA phase (its last
+      // reader, reduce_store of tile v - 1, ran before barrier 1); 2 x 256 B per wave
+      float* ab = reinterpret_cast<float*>(red0 + tpar * 4 * 64) + wave * 128;
       sl_light<KF>(da, d0, kmax, slope, dp, seed, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid,
-                   r0, erg, lane);
+                   r0, erg, ab, lane);
       sl_light<KF>(db, d1, kmax, slope, dp, seed, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid,
-                   r1, erg, lane);
+                   r1, erg, ab + 64, lane);
     } else {
       sl_general<XT, KF, NL, NA>(rg + r0, d0, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
                                  stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane);
@@ -584,7 +634,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       if (u < KH) {
         const f16x8 ahi = phi[u % kAP], alo = plo[u % kAP];
         f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % kAP];
+#ifdef GFD_AB_LIGHT_NOAREAD  // ablation only (wrong results): A fragments of k-step 0 reused
+        if (!LIGHT && u + kAP < KH) {
+#else
         if (u + kAP < KH) {
+#endif
           phi[u % kAP] = *reinterpret_cast<const f16x8*>(ah + 32 * (u + kAP));
           plo[u % kAP] = *reinterpret_cast<const f16x8*>(al + 32 * (u + kAP));
           if (u + kAP >= NR) {
@@ -593,9 +647,16 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
           }
         }
         f32x4& acc = (u & 1) ? acc1 : acc0;
+#ifdef GFD_AB_LIGHT_NOMFMA  // ablation only (wrong results): no MFMAs, operands consumed
+        if (LIGHT) {
+          acc[0] += float(ahi[0]) + float(alo[1]) + float(bh[u][2]) + float(blo[3]);
+        } else
+#endif
+        {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[u], acc, 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }

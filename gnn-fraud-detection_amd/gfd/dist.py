@@ -784,3 +784,120 @@ def model_forward_sharded(model, x: torch.Tensor, graph, spec: ShardSpec, group=
     if gather_output and spec.world > 1:
         return all_gather_v_rows(out, spec.dst_bounds, group=group)
     return out
+
+
+# ---------------------------------------------------------------------------
+# Sharded training (train.py:115-143 on the destination-sharded variant).
+#
+# Rank r owns destinations [lo, hi) and therefore every message into them
+# (their segment softmax is rank-local).  Its share of a GATConv layer's
+# forward AND backward runs on a LOCAL subgraph: the own destinations (rows
+# 0 .. n_dst - 1, their CSR rows verbatim: input edges, self loop last) plus
+# the sources those messages read from other blocks (rows n_dst ..; their
+# only message is their own self loop, PyG's policy).  The local forward
+# computes the halo rows' logits itself (x is resident on every rank: no
+# exchange for layer 0) and the own rows' outputs exactly as the whole-graph
+# forward does; the halo rows' outputs are not used, so their output
+# gradient is zero and they add nothing to the backward, whose destination
+# pass covers the own messages and whose source pass and grad_W' GEMM cover
+# only the local rows -- the sources with local out-edges, not all N.  The
+# parameter gradients of the ranks are partial sums of the whole-graph ones
+# (every message belongs to exactly one rank), so ONE all-reduce of the
+# layer's 0.35 MB of gradients completes them (``all_reduce_grads``).
+# Dropout: the counter-based masks are keyed by CSR position, local here, so
+# a sharded step draws different (equally distributed) masks than a
+# single-process one.
+
+class LocalGraph:
+    """Rank-local subgraph of a destination shard (module section above).
+
+    ``nodes`` -- int64 [N_loc] global id of each local row (own destinations
+    ``lo .. hi - 1`` first, then the halo sources in ascending order);
+    ``graph`` -- the local CSRGraph (PyG self-loop policy); ``n_dst``."""
+
+    def __init__(self, nodes: torch.Tensor, graph, n_dst: int, lo: int, hi: int):
+        self.nodes, self.graph, self.n_dst, self.lo, self.hi = nodes, graph, n_dst, lo, hi
+        self._x_key = None
+        self._x_loc = None
+
+    @property
+    def num_halo(self) -> int:
+        return int(self.nodes.numel()) - self.n_dst
+
+    def rows(self, x: torch.Tensor) -> torch.Tensor:
+        """x's local rows (own block, then halo), through autograd when x
+        requires grad; a constant x (layer 0's features) is gathered once per
+        (storage, version) and kept."""
+        if x.requires_grad:
+            return x.index_select(0, self.nodes)
+        key = (x.data_ptr(), x._version, tuple(x.shape), x.stride(0), x.dtype)
+        if self._x_key != key:
+            src = x if x.stride(1) == 1 else x.contiguous()
+            self._x_loc = src.index_select(0, self.nodes)
+            self._x_key = key
+        return self._x_loc
+
+
+def local_graph(graph, lo: int, hi: int) -> LocalGraph:
+    """The LocalGraph of destinations [lo, hi) of ``graph`` (a CSRGraph on any
+    device; CPU graphs serve the gloo tests).  Built once per range and cached
+    on the graph (one host sync when built)."""
+    cache = getattr(graph, "_local", None)
+    key = (int(lo), int(hi))
+    if cache is not None and key in cache:
+        return cache[key]
+    from .graph import CSRGraph
+    rp = graph.rowptr
+    dev = rp.device
+    e0, e1 = int(rp[lo].item()), int(rp[hi].item())
+    col = graph.col[e0:e1].to(torch.int64)
+    n_dst = hi - lo
+    halo = torch.unique(col[(col < lo) | (col >= hi)])          # sorted
+    nodes = torch.cat([torch.arange(lo, hi, dtype=torch.int64, device=dev), halo])
+    n_loc = int(nodes.numel())
+    gmap = torch.full((graph.num_nodes,), -1, dtype=torch.int64, device=dev)
+    gmap[nodes] = torch.arange(n_loc, dtype=torch.int64, device=dev)
+    n_halo = n_loc - n_dst
+    m_own = e1 - e0
+    rowptr = torch.cat([rp[lo:hi + 1].to(torch.int64) - e0,
+                        m_own + torch.arange(1, n_halo + 1, dtype=torch.int64, device=dev)])
+    lcol = torch.cat([gmap[col], torch.arange(n_dst, n_loc, dtype=torch.int64, device=dev)])
+    g = CSRGraph(n_loc, rowptr.to(torch.int32), lcol.to(torch.int32), m_own + n_halo,
+                 m_own - n_dst)
+    lg = LocalGraph(nodes, g, n_dst, lo, hi)
+    if hasattr(graph, "_shards"):
+        if cache is None:
+            cache = {}
+            graph._local = cache
+        cache[key] = lg
+    return lg
+
+
+def gat_conv_local(x: torch.Tensor, local: LocalGraph, weight: torch.Tensor,
+                   att_src: torch.Tensor, att_dst: torch.Tensor, bias: Optional[torch.Tensor],
+                   negative_slope: float = 0.2, dropout: float = 0.0,
+                   training: bool = False) -> torch.Tensor:
+    """This rank's share of a GATConv forward with autograd: the ``[n_dst, 64]``
+    outputs of its destinations, computed on the LocalGraph (gfd_gat_fwd /
+    gfd_gat_bwd on the local rows).  After ``backward`` the parameter
+    gradients hold this rank's partial sums: ``all_reduce_grads``."""
+    from .nn import gat_conv
+    out = gat_conv(local.rows(x), local.graph, weight, att_src, att_dst, bias,
+                   negative_slope=negative_slope, dropout=dropout, training=training)
+    return out[:local.n_dst]
+
+
+def all_reduce_grads(params, group=None) -> None:
+    """Sum the ranks' partial parameter gradients (one flat all-reduce; the
+    reference layer's W, att_src, att_dst, bias: 0.35 MB at F = 166)."""
+    import torch.distributed as dist
+    ps = [p for p in params if p.grad is not None]
+    if not ps or dist.get_world_size(group) == 1:
+        return
+    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    dist.all_reduce(flat, group=group)
+    off = 0
+    for p in ps:
+        n = p.grad.numel()
+        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        off += n

@@ -1,0 +1,109 @@
+"""Sharded training step of a GATConv layer on CPU with gloo (train.py:115-143
+on the destination-sharded variant; gfd.dist "Sharded training").
+
+Each rank builds the LocalGraph of its destination shard (own destinations,
+then the halo sources with only their self loop), runs the layer forward and
+backward on it (oracle arithmetic in place of the HIP kernels, which need a
+GPU; tests/test_dist_gpu.py runs the kernels), and the partial parameter
+gradients are all-reduced: the result must equal the single-process
+gradients of the whole graph."""
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from _util import assert_close_scaled, csr_cpu
+from test_dist_cpu import _problem, _store_path, N, H, C
+from gfd import dist as gdist
+from gfd.graph import CSRGraph
+from oracle import gatconv_ref as ref
+
+
+def _graph_cpu(ei):
+    rowptr, col = csr_cpu(ei, N)
+    return CSRGraph(N, rowptr.to(torch.int32), col.to(torch.int32), int(rowptr[-1]), ei.size(1))
+
+
+def _local_coo(lg):
+    """The LocalGraph's messages as a COO edge list without self loops (the
+    oracle re-adds one per node, as the local CSR holds)."""
+    rp, col = lg.graph.rowptr.long(), lg.graph.col.long()
+    n = lg.graph.num_nodes
+    dst = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+    keep = col != dst
+    return torch.stack([col[keep], dst[keep]])
+
+
+def _grad_out():
+    return torch.randn(N, C, generator=torch.Generator().manual_seed(9))
+
+
+def _train_rank(rank, world, path, balance, q):
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
+    try:
+        ei, x, W, a_s, a_d, b = _problem()
+        g = _graph_cpu(ei)
+        spec = gdist.ShardSpec(g.rowptr.long(), rank, world, balance)
+        lg = gdist.local_graph(g, spec.dst_lo, spec.dst_hi)
+        params = [t.clone().requires_grad_(True) for t in (W, a_s, a_d, b)]
+        x_loc = lg.rows(x)
+        out = ref.gatconv_forward(x_loc, _local_coo(lg), *params, heads=H)[:lg.n_dst]
+        (out * _grad_out()[spec.dst_lo:spec.dst_hi]).sum().backward()
+        gdist.all_reduce_grads(params)
+        if rank == 0:
+            q.put(([p.grad.numpy() for p in params], lg.graph.num_nodes, lg.n_dst))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,balance", [(2, "messages"), (3, "cost"), (2, "nodes")])
+def test_sharded_train_step_matches_single_process(world, balance):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = _store_path()
+    procs = [ctx.Process(target=_train_rank, args=(r, world, path, balance, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    grads, n_loc, n_dst = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ei, x, W, a_s, a_d, b = _problem()
+    params = [t.clone().requires_grad_(True) for t in (W, a_s, a_d, b)]
+    out = ref.gatconv_forward(x, ei, *params, heads=H)
+    (out * _grad_out()).sum().backward()
+    for name, got, p in zip(("W", "att_src", "att_dst", "bias"), grads, params):
+        assert_close_scaled(torch.from_numpy(got), p.grad, rtol=2e-5,
+                            what=f"sharded {name} grad, world {world} ({balance})")
+    assert n_dst < N and n_loc < N + 1   # rank 0's local rows: own block + halo, not all N
+
+
+def test_local_graph_structure():
+    ei, x, *_ = _problem()
+    g = _graph_cpu(ei)
+    rowptr = g.rowptr.long()
+    deg = rowptr[1:] - rowptr[:-1]
+    for lo, hi in ((0, 200), (150, 420), (480, N)):
+        lg = gdist.local_graph(g, lo, hi)
+        nodes = lg.nodes
+        assert torch.equal(nodes[:hi - lo], torch.arange(lo, hi))
+        assert nodes.unique().numel() == nodes.numel()
+        lrp = lg.graph.rowptr.long()
+        ldeg = lrp[1:] - lrp[:-1]
+        # own rows keep every message in order (global ids through the node map)
+        assert torch.equal(ldeg[:hi - lo], deg[lo:hi])
+        own = lg.graph.col[:int(lrp[hi - lo])].long()
+        assert torch.equal(nodes[own], g.col[int(rowptr[lo]):int(rowptr[hi])].long())
+        # halo rows: their own self loop only, and exactly the sources read
+        assert bool((ldeg[hi - lo:] == 1).all())
+        halo_col = lg.graph.col[int(lrp[hi - lo]):].long()
+        assert torch.equal(halo_col, torch.arange(hi - lo, nodes.numel()))
+        src = g.col[int(rowptr[lo]):int(rowptr[hi])].long()
+        want = torch.unique(src[(src < lo) | (src >= hi)])
+        assert torch.equal(nodes[hi - lo:], want)
+        assert lg.graph.num_messages == int(lrp[-1])
+        # constant x: gathered once per version
+        a = lg.rows(x)
+        assert lg.rows(x) is a and torch.equal(a, x[nodes])
