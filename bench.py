@@ -68,6 +68,8 @@ def parse(argv=None):
                         "rank 2.03 ms against 2.06 for equal node blocks), equal node blocks "
                         "(C4's ids are randomly permuted: messages within 2.6 %% at 8 ranks) "
                         "or message-balanced ranges")
+    p.add_argument("--overlap", action="store_true",
+                   help="run the light class on a second stream beside hubs -> general")
     p.add_argument("--exchange", choices=["halo", "halo1", "allgather"], default="halo",
                    help="N > 1 source-logits exchange: each rank receives only the rows its "
                         "messages read (RCCL all-to-all; ~22 %% of the other ranks' nodes at "
@@ -83,7 +85,7 @@ def parse(argv=None):
                         "8-float slot in every x row")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-legs", action="store_true")
-    p.add_argument("--legs", default="c4bwd,sample,c5,c1,c2,c3,temporal,ingest",
+    p.add_argument("--legs", default="c4bwd,dropin,sample,c5,c1,c2,c3,temporal,ingest",
                    help="comma list of legs run after the headline line (N = 1)")
     p.add_argument("--legs-only", action="store_true",
                    help="skip the C4 headline timing (development)")
@@ -174,7 +176,15 @@ class Layer:
             self.N, self.n_dst, F, H, C, self.plan.num_hubs, self.plan.num_chunks),
             dtype=torch.uint8, device=dev)
         self.xmax = torch.zeros(1, dtype=torch.float32, device=dev)
+        # max |x| over ALL rows (the tile stage's one Z-row scale) is a property
+        # of the input, like the CSR and the plan: computed by the first step's
+        # logits passes and all-reduced once per x version, then kept
+        # (it was all-reduced every step)
+        self._xmax_key = None
         self.stream = _lib.stream_handle(dev)
+        self.overlap = False   # --overlap (set by measure): light on a second stream
+        self.side = torch.cuda.Stream(device=dev)
+        self._ready = torch.cuda.Event()
         self.cplan = self.plan.cstruct()
         # the lone destinations' outputs come out of the logits pass
         # (gfd_gat_logits_lone over the rank's destinations) and the tile stage
@@ -211,7 +221,8 @@ class Layer:
         s, _lib, F = self.s, self._lib, self.s["F"]
         _lib.call("gfd_gat_pack_weights", s["W"].data_ptr(), s["a_s"].data_ptr(),
                   s["a_d"].data_ptr(), F, H, C, self.packed.data_ptr(), self.stream)
-        self.xmax.zero_()
+        if not self.xmax_current():
+            self.xmax.zero_()   # (kept: the passes' atomic max of the same rows changes nothing)
         x, spec = s["x"], s["spec"]
         if self.in_row:
             _lib.call("gfd_gat_logits_lone_split", x.data_ptr(), self.xdt, self.N, F, s["ldx"],
@@ -255,12 +266,18 @@ class Layer:
             return
         logits(0, n)
 
+    def xmax_current(self) -> bool:
+        x = self.s["x"]
+        return self._xmax_key == (x.data_ptr(), x._version)
+
     def exchange(self):
         # ONE all-gather-v of the [N, 8] source logits (RCCL; uneven blocks land
-        # at their node rows) and the max |x| reduction the tile stage's row
-        # scale needs
+        # at their node rows) and, once per x version, the max |x| reduction the
+        # tile stage's row scale needs
         import torch.distributed as dist
         r = self.s["spec"].rank
+        reduce_xmax = not self.xmax_current()
+        self._xmax_key = (self.s["x"].data_ptr(), self.s["x"]._version)
         if self.halo is not None:
             # the rows this shard reads, straight into s_all (gfd_rows_copy pack,
             # RCCL all-to-all, gfd_rows_copy scatter; gloo: host-staged); the
@@ -271,6 +288,8 @@ class Layer:
                 self.pending = []
             else:
                 self.halo.exchange(self.s_all)
+            if not reduce_xmax:
+                return
             if dist.get_backend() == "gloo":
                 xm = self.xmax.cpu()
                 dist.all_reduce(xm, op=dist.ReduceOp.MAX)
@@ -279,15 +298,16 @@ class Layer:
                 dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
             return
         if dist.get_backend() == "gloo":   # --rehearse: the same exchange, host-staged
-            if not self.equal:
-                raise RuntimeError("--rehearse supports the node-balanced (equal-block) exchange")
-            per = self.s_blocks[0].shape[0]
-            cpu = self.s_all[:len(self.s_blocks) * per].cpu()
-            dist.all_gather_into_tensor(cpu, cpu[r * per:(r + 1) * per].clone())
-            self.s_all[:len(self.s_blocks) * per].copy_(cpu)
-            xm = self.xmax.cpu()
-            dist.all_reduce(xm, op=dist.ReduceOp.MAX)
-            self.xmax.copy_(xm)
+            # (equal blocks: one in-place all-gather; uneven blocks, e.g. the
+            # default cost balance: gather_blocks' padded gloo path -- ADVICE r4)
+            from gfd import dist as gdist
+            cpu = self.s_all.cpu()
+            gdist.gather_blocks(cpu, self.s["spec"])
+            self.s_all.copy_(cpu)
+            if reduce_xmax:
+                xm = self.xmax.cpu()
+                dist.all_reduce(xm, op=dist.ReduceOp.MAX)
+                self.xmax.copy_(xm)
             return
         if self.equal:
             # s_all IS the gathered layout: in place, one RCCL all-gather
@@ -295,17 +315,19 @@ class Layer:
                                         self.s_blocks[r])
         else:  # uneven blocks (RCCL grouped broadcasts into the row views)
             dist.all_gather(self.s_blocks, self.s_blocks[r])
-        dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
+        if reduce_xmax:
+            dist.all_reduce(self.xmax, op=dist.ReduceOp.MAX)
 
-    def aggregate(self, stages):
+    def aggregate(self, stages, stream=None):
         s = self.s
+        st_h = self.stream if stream is None else stream
         if self.in_row:
             self._lib.call("gfd_gat_aggregate_split", s["x"].data_ptr(), self.xdt, self.N, s["F"],
                            s["ldx"], s["shard"].rowptr.data_ptr(), s["graph"].col.data_ptr(),
                            self.n_dst, 0, self.s_ptr, self.lds, self.t_loc.data_ptr(), H,
                            self.xmax.data_ptr(), self.packed.data_ptr(), s["bias"].data_ptr(), H,
                            C, 0.2, 0.0, 0, self.cplan, stages, None, self.out.data_ptr(), C, None,
-                           self.ws.data_ptr(), self.ws.numel(), self.stream)
+                           self.ws.data_ptr(), self.ws.numel(), st_h)
             return
         if self.whole:
             self._lib.call("gfd_gat_aggregate_ex", s["x"].data_ptr(), self.xdt, self.N, s["F"],
@@ -313,7 +335,7 @@ class Layer:
                            self.n_dst, 0, self.st.data_ptr(), self.xmax.data_ptr(),
                            self.packed.data_ptr(), s["bias"].data_ptr(), H, C, 0.2, 0.0, 0,
                            self.cplan, stages, self.out.data_ptr(), None, self.ws.data_ptr(),
-                           self.ws.numel(), self.stream)
+                           self.ws.numel(), st_h)
             return
         self._lib.call("gfd_gat_aggregate_split", s["x"].data_ptr(), self.xdt, self.N, s["F"],
                        s["ldx"], s["shard"].rowptr.data_ptr(), s["graph"].col.data_ptr(),
@@ -329,26 +351,55 @@ class Layer:
                       ("general", STAGE_MID), ("light", STAGE_LIGHT))
 
     def step(self, evs=None):
+        """One layer forward.  ``evs`` (timing): a dict filled with one
+        (start, end) event pair per stage name, recorded on the stream the
+        stage's launches go to."""
         # events record on torch's current stream == the stream every gfd launch
         # uses (and the one RCCL's collectives are ordered against)
-        for k, (_, stg) in enumerate(self.stages):
-            if evs:
-                evs[k].record()
+        main = torch.cuda.current_stream(self.dev)
+
+        def run(name, stg, stream=None):
+            ev = None
+            if evs is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(stream or main)
             if stg is None:
                 self.pack_and_logits()
             elif stg == "x":
                 self.exchange()
             else:
-                self.aggregate(stg)
-        if evs:
-            evs[-1].record()
+                self.aggregate(stg, None if stream is None else stream.cuda_stream)
+            if ev is not None:
+                ev[1].record(stream or main)
+                evs[name] = ev
+
+        if not self.overlap:
+            for name, stg in self.stages:
+                run(name, stg)
+            return
+        # --overlap: the light class on a second stream once the logits (and
+        # the exchange) are in, beside hubs -> general on the main stream (the
+        # three tile launches are independent but for general reading the hub
+        # rows' merged z), so light's blocks take the CUs general's tail frees.
+        # Each stage's span is timed on its own stream; the step ends when both
+        # streams are done.
+        for name, stg in self.stages:
+            if stg is None or stg == "x":
+                run(name, stg)
+        self._ready.record(main)
+        self.side.wait_event(self._ready)
+        with torch.cuda.stream(self.side):
+            run("light", STAGE_LIGHT, self.side)
+        for name, stg in self.stages:
+            if stg in (STAGE_HUBS, STAGE_MID):
+                run(name, stg)
+        main.wait_stream(self.side)
 
 
 def time_layer(layer, steps, warmup, world):
     for _ in range(warmup):
         layer.step()
-    nst = len(layer.stages)
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(nst + 1)] for _ in range(steps)]
+    events = [{} for _ in range(steps)]
     torch.cuda.synchronize()
     if world > 1:
         import torch.distributed as dist
@@ -363,8 +414,8 @@ def time_layer(layer, steps, warmup, world):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
-    stage_ms = {name: med([e[k].elapsed_time(e[k + 1]) for e in events])
-                for k, (name, _) in enumerate(layer.stages)}
+    stage_ms = {name: med([e[name][0].elapsed_time(e[name][1]) for e in events])
+                for name, _ in layer.stages}
     mine = elapsed
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=layer.dev)
@@ -498,6 +549,7 @@ def measure(args, dev, rank, world, config):
     s = setup(dev, N, E, F, args.gamma, dtype, rank, world, row_align=row_align,
               balance=args.balance, s_in_row=not args.no_s_in_row)
     layer = Layer(s, dev, world, getattr(args, "exchange", "halo"))
+    layer.overlap = bool(getattr(args, "overlap", False))
     plan = layer.plan
     esz = s["xbuf"].element_size()
     log(f"[bench] {config} rank {rank}/{world}: N={N} E={E} messages={s['graph'].num_messages} "
@@ -661,6 +713,9 @@ def main():
             legs["c4_layer_fwd_bwd"] = leg
             log("[bench] leg C4 forward + backward, attention dropout 0.2 ...")
             legs["c4_layer_fwd_bwd_dropout"] = bench_legs.c4_layer_fwd_bwd(s, dev, dropout=0.2)
+        if "dropin" in want:
+            log("[bench] leg drop-in module (gfd.nn.GATConv on the COO edge_index) ...")
+            legs["c4_dropin_module"] = bench_legs.dropin_module(s, dev, res["ms_per_step"])
         if "sample" in want:
             log("[bench] leg neighbour sampling on the C4 graph ...")
             legs["neighbor_sampling"] = bench_legs.neighbor_sampling(s, dev)

@@ -10,7 +10,9 @@
 // entry point returns GFD_ERR_INDEX before any gather kernel is launched,
 // instead of a kernel faulting somewhere inside a gather.  This build
 // synchronises the stream once per call to read the record (the product
-// library never does).  The product library contains none of this.
+// library never does), and its one record per device makes concurrent calls
+// from several host threads serialise on a host mutex.  The product library
+// contains none of this.
 #pragma once
 
 #include "gfd_common.h"

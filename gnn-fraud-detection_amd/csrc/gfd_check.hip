@@ -1,5 +1,7 @@
 // gfd_check.hip -- device validation of the index arrays (the bounds-checked
 // diagnostic build, gfd_check.h).  Compiled to a no-op without GFD_CHECKED.
+#include <mutex>
+
 #include "gfd_check.h"
 
 namespace gfd {
@@ -71,6 +73,11 @@ gfd_status check_graph(const int32_t* rowptr, const int32_t* col, int64_t num_ds
                        const gfd_plan* plan, const int32_t* colptr, const int32_t* csc_dst,
                        const int32_t* csc_eid, int64_t num_messages, hipStream_t stream) {
 #ifdef GFD_CHECKED
+  // one record per device: calls on other streams (per-rank threads, the
+  // sampler's stream) would clear or read each other's -- the checked build
+  // serialises check_graph across host threads
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
   void* rec = nullptr;
   if (hipGetSymbolAddress(&rec, HIP_SYMBOL(g_check)) != hipSuccess) return GFD_ERR_HIP;
   if (hipMemsetAsync(rec, 0, sizeof(CheckRecord), stream) != hipSuccess) return GFD_ERR_HIP;

@@ -13,13 +13,20 @@
 // k_logits_lone: one 16-wave block per CU, grid-stride over 16-row tiles.
 //   * lane (r = l & 15, g = l >> 4) loads features 16 s + 4 g .. +3 of row r
 //     for every fp32 k-step s (fp32), or 32 t + 8 g .. +7 for every f16
-//     k-step t (bf16) -- 16-B loads, all issued before the first MFMA;
+//     k-step t (bf16) -- 16-B loads (pairs of 8-B loads for rows that are only
+//     8-B aligned, e.g. a contiguous [N, 166] fp32 x), all issued before the
+//     first MFMA;
 //   * the row, scaled by 2^e (max |x| -> [2^13, 2^14)), is split into f16
 //     hi / lo' once per f16 k-step t (fp32 k-steps 2 t and 2 t + 1 of the
 //     lane, matched by the permuted fragments of k_pack_wbar_perm /
 //     k_pack_uv_perm, which stay in LDS for the launch);
 //   * st = x . [U | V] on v_mfma_f32_16x16x32_f16 (3-term split, ~2^-21
 //     relative: 18 MFMAs per tile instead of 44 fp32 16x16x4 ones);
+//   * a tile holding a row whose nonzero features span more than 2^18 (an
+//     outlier feature: under one row scale the f16 split would lose the small
+//     ones -- tests/test_gatconv_gpu.py::test_backward_heavy_tailed_features)
+//     takes fp32 MFMA instead, with the same fragments as fp32 B operands
+//     (hi + lo): exact fp32 products for its logits and lone outputs;
 //   * if any row of the tile is lone: out = x . Wbar^T from the same
 //     fragments (12 more MFMAs per k-step);
 //   * out rows (and, in training, the softmax stats: max = leaky(s_i + t_i),
@@ -54,12 +61,13 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <typename XT, int KS, bool HEAD>
+template <typename XT, int KS, bool HEAD, bool A16>
 __global__ void __launch_bounds__(kLLWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_logits_lone(
     const typename XT::T* __restrict__ x, int64_t rows, int F, int64_t ldx,
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ uph,
-    const uint4* __restrict__ upl, const uint4* __restrict__ wph, const uint4* __restrict__ wpl,
+    const uint4* __restrict__ upl,
+    const uint4* __restrict__ wph, const uint4* __restrict__ wpl,
     const int32_t* __restrict__ rowptr, const float* __restrict__ bias, float slope,
     float* __restrict__ sl, int lds, float* __restrict__ tl, int ldt, float* __restrict__ xmax,
     float* __restrict__ out,
@@ -115,14 +123,21 @@ k_logits_lone(
     constexpr bool kH = XT::kBytes == 2;
     f32x4 a[kH ? 1 : kLKS];
     uint4 hb[kH ? kLKB : 1];
-    float rm = 0.f;  // max |x| of this lane's part of the row
+    float rm = 0.f;         // max |x| of this lane's part of the row
+    float rmin = INFINITY;  // and its smallest nonzero |x|
     if constexpr (kH) {
       const uint16_t* xh = reinterpret_cast<const uint16_t*>(x) + (rin ? row : rows - 1) * ldx + 8 * g;
 #pragma unroll
       for (int tt = 0; tt < kLKB; ++tt) {
         const int f0 = 32 * tt + 8 * g;
         if (tt < KB && f0 + 8 <= F) {
-          hb[tt] = *reinterpret_cast<const uint4*>(xh + 32 * tt);
+          if constexpr (A16) {
+            hb[tt] = *reinterpret_cast<const uint4*>(xh + 32 * tt);
+          } else {  // 8-B aligned rows (a row pitch of 4 k bf16): two 8-B loads
+            const uint2 u0 = *reinterpret_cast<const uint2*>(xh + 32 * tt);
+            const uint2 u1 = *reinterpret_cast<const uint2*>(xh + 32 * tt + 4);
+            hb[tt] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+          }
         } else {  // ragged tail: guarded scalar loads (never past the row)
           uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -135,9 +150,12 @@ k_logits_lone(
       for (int tt = 0; tt < kLKB; ++tt) {
         const uint32_t w[4] = {hb[tt].x, hb[tt].y, hb[tt].z, hb[tt].w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          rm = fmaxf(rm, fmaxf(fabsf(__uint_as_float(w[i] << 16)),
-                               fabsf(__uint_as_float(w[i] & 0xffff0000u))));
+        for (int i = 0; i < 4; ++i) {
+          const float v0 = fabsf(__uint_as_float(w[i] << 16));
+          const float v1 = fabsf(__uint_as_float(w[i] & 0xffff0000u));
+          rm = fmaxf(rm, fmaxf(v0, v1));
+          rmin = fminf(rmin, fminf(v0 > 0.f ? v0 : INFINITY, v1 > 0.f ? v1 : INFINITY));
+        }
       }
     } else {
       const typename XT::T* xr = x + (rin ? row : rows - 1) * ldx + 4 * g;
@@ -155,7 +173,13 @@ k_logits_lone(
 #ifdef GFD_AB_LOGITS_COAL
           a[s] = load4<XT>(xc + 256 * s);
 #else
-          a[s] = load4<XT>(xr + 16 * s);
+          if constexpr (A16) {
+            a[s] = load4<XT>(xr + 16 * s);
+          } else {  // 8-B aligned rows (an even row pitch: the reference's [N, 166]): two 8-B loads
+            const float2 u0 = *reinterpret_cast<const float2*>(xr + 16 * s);
+            const float2 u1 = *reinterpret_cast<const float2*>(xr + 16 * s + 2);
+            a[s] = f32x4{u0.x, u0.y, u1.x, u1.y};
+          }
 #endif
         } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
 #pragma unroll
@@ -165,8 +189,14 @@ k_logits_lone(
         }
       }
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        rm = fmaxf(fmaxf(rm, fmaxf(fabsf(a[s].x), fabsf(a[s].y))), fmaxf(fabsf(a[s].z), fabsf(a[s].w)));
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float v = fabsf(a[s][u]);
+          rm = fmaxf(rm, v);
+          rmin = fminf(rmin, v > 0.f ? v : INFINITY);
+        }
+      }
     }
     const bool lone = rin && rowptr[row + 1] - rowptr[row] == 1;
     am = fmaxf(am, rm);  // clamped tail rows repeat row rows - 1: harmless for a max
@@ -175,46 +205,98 @@ k_logits_lone(
 #else
     const bool any_lone = __ballot(lone) != 0;  // wave-uniform
 #endif
-    const int er = scale_exp(max_xor16_32(rm));  // lanes r, r + 16, r + 32, r + 48
+    // Row conditioning: a row whose smallest nonzero |x| is below 2^-18 of its
+    // max has features the one-row-scale f16 split cannot hold to ~2^-21 (an
+    // outlier feature); a tile with such a row runs on fp32 MFMA (wave-uniform)
+    const float rmax_row = max_xor16_32(rm);                 // lanes r, r + 16, r + 32, r + 48
+    const float rmin_row = -max_xor16_32(-rmin);
+    const bool ill = rin && rmin_row < rmax_row * 0x1p-18f;
+    const bool exact = __ballot(ill) != 0;                    // wave-uniform
+    const int er = exact ? 0 : scale_exp(rmax_row);
     const float rs = ldexpf(1.0f, er);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     f32x4 o[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int tt = 0; tt < kLKB; ++tt) {
-      if (tt >= KB) break;  // uniform: past the row's k-steps
-      union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f32x2 v;
-        if constexpr (kH) {
-          const uint32_t w = i == 0 ? hb[tt].x : i == 1 ? hb[tt].y : i == 2 ? hb[tt].z : hb[tt].w;
-          v = f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)} * f32x2{rs, rs};
-        } else {
-          const f32x4& src = a[2 * tt + (i >> 1)];
-          v = f32x2{src[2 * (i & 1)], src[2 * (i & 1) + 1]} * f32x2{rs, rs};
-        }
-        hi.p[i] = __builtin_convertvector(v, f16x2);
-        lo.u[i] = split_lo(v, hi.u[i]);
+    // the lane's K value at position j (0..7) of f16 k-step tt, unscaled fp32
+    // (fp32 x: the permuted order -- j < 4: fp32 k-step 2 tt, j >= 4: 2 tt + 1;
+    // bf16 x: the plain order of the lane's 8-feature load)
+    auto xk = [&](int tt, int j) -> float {
+      if constexpr (kH) {
+        const uint32_t w = (j >> 1) == 0 ? hb[tt].x : (j >> 1) == 1 ? hb[tt].y
+                         : (j >> 1) == 2 ? hb[tt].z : hb[tt].w;
+        return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
+      } else {
+        return a[2 * tt + (j >> 2)][j & 3];
       }
-      {
+    };
+    if (exact) {
+      // fp32 MFMA 16x16x4: the lane's j-th K value against the fragments'
+      // j-th entry (hi + lo: the packed fp32-faithful value), 8 MFMAs per
+      // f16 k-step and 16-column tile, two accumulator chains each
+      f32x4 acc2 = acc;
+      f32x4 o2[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) o2[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tt = 0; tt < kLKB; ++tt) {
+        if (tt >= KB) break;  // uniform: past the row's k-steps
         const uint4 uh = UP[0][tt][lane], ul = UP[1][tt][lane];
         const f16x8 u_h = *reinterpret_cast<const f16x8*>(&uh);
         const f16x8 u_l = *reinterpret_cast<const f16x8*>(&ul);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_h, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_l, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, u_h, acc, 0, 0, 0);
-      }
-      if (any_lone) {
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
-          const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
-          const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
-          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, o[ct], 0, 0, 0);
-          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, o[ct], 0, 0, 0);
-          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, o[ct], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) {
+          f32x4& ac = (j & 1) ? acc2 : acc;
+          ac = __builtin_amdgcn_mfma_f32_16x16x4f32(xk(tt, j), float(u_h[j]) + float(u_l[j]), ac,
+                                                   0, 0, 0);
+        }
+        if (any_lone) {
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) {
+            const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
+            const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+            const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              f32x4& oc = (j & 1) ? o2[ct] : o[ct];
+              oc = __builtin_amdgcn_mfma_f32_16x16x4f32(xk(tt, j), float(b_h[j]) + float(b_l[j]),
+                                                       oc, 0, 0, 0);
+            }
+          }
+        }
+      }
+      acc += acc2;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) o[ct] += o2[ct];
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < kLKB; ++tt) {
+        if (tt >= KB) break;  // uniform: past the row's k-steps
+        union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x2 v = f32x2{xk(tt, 2 * i), xk(tt, 2 * i + 1)} * f32x2{rs, rs};
+          hi.p[i] = __builtin_convertvector(v, f16x2);
+          lo.u[i] = split_lo(v, hi.u[i]);
+        }
+        {
+          const uint4 uh = UP[0][tt][lane], ul = UP[1][tt][lane];
+          const f16x8 u_h = *reinterpret_cast<const f16x8*>(&uh);
+          const f16x8 u_l = *reinterpret_cast<const f16x8*>(&ul);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_h, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_l, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, u_h, acc, 0, 0, 0);
+        }
+        if (any_lone) {
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) {
+            const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
+            const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+            const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+            o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, o[ct], 0, 0, 0);
+            o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, o[ct], 0, 0, 0);
+            o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, o[ct], 0, 0, 0);
+          }
         }
       }
     }
@@ -347,8 +429,17 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
   int64_t nb = (tiles + kLLWaves - 1) / kLLWaves;
   const int64_t cap = int64_t(cu_count());  // resident blocks; grid-stride beyond
   if (nb > cap) nb = cap;
-  auto kern = ep.hout ? (F <= 176 ? &k_logits_lone<XT, 11, true> : &k_logits_lone<XT, 12, true>)
-                      : (F <= 176 ? &k_logits_lone<XT, 11, false> : &k_logits_lone<XT, 12, false>);
+  const uintptr_t xa = reinterpret_cast<uintptr_t>(x);
+  const bool a16 = xa % 16 == 0 && (ldx * XT::kBytes) % 16 == 0;
+  const bool k11 = F <= 176;
+  auto kern = a16 ? (ep.hout ? (k11 ? &k_logits_lone<XT, 11, true, true>
+                                    : &k_logits_lone<XT, 12, true, true>)
+                             : (k11 ? &k_logits_lone<XT, 11, false, true>
+                                    : &k_logits_lone<XT, 12, false, true>))
+                  : (ep.hout ? (k11 ? &k_logits_lone<XT, 11, true, false>
+                                    : &k_logits_lone<XT, 12, true, false>)
+                             : (k11 ? &k_logits_lone<XT, 11, false, false>
+                                    : &k_logits_lone<XT, 12, false, false>));
   const size_t smem = sizeof(uint4) * 2 * kLKB * 5 * 64 + sizeof(float) * 2 * C +
                       sizeof(float) * kLLWaves * 16 * kTP;
   if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
@@ -371,10 +462,11 @@ namespace gfd {
 namespace fwd {
 
 bool logits_lone_supported(const void* x, int xdt, int F, int64_t ldx) {
-  // fp32: 16-B loads of 4 features; bf16: 16-B loads of 8
+  // fp32: 16-B loads of 4 features; bf16: 16-B loads of 8 -- or, for rows
+  // only 8-B aligned (the reference's contiguous [N, 166] fp32 x), two 8-B loads
   const uintptr_t a = reinterpret_cast<uintptr_t>(x);
-  const int per = xdt == GFD_DTYPE_BF16 ? 8 : 4;
-  return F >= 1 && F <= 16 * kLKS && a % 16 == 0 && ldx % per == 0;
+  const int per = xdt == GFD_DTYPE_BF16 ? 4 : 2;
+  return F >= 1 && F <= 16 * kLKS && a % 8 == 0 && ldx % per == 0;
 }
 
 gfd_status launch_logits_lone(const void* x, int xdt, int64_t rows, int F, int64_t ldx,

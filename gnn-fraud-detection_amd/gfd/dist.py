@@ -711,10 +711,24 @@ def shard_columns(graph, spec: ShardSpec) -> torch.Tensor:
     return col[int(rowptr[spec.dst_lo]):int(rowptr[spec.dst_hi])]
 
 
+def _group_key(group):
+    """A process group by what the halo plan depends on -- its backend and
+    member ranks -- not by ``id()``, which a destroyed group's successor may
+    reuse."""
+    import torch.distributed as dist
+    g = group if group is not None else dist.group.WORLD
+    try:
+        ranks = tuple(dist.get_process_group_ranks(g))
+    except Exception:  # noqa: BLE001 -- older torch: world size and rank only
+        ranks = (dist.get_world_size(group), dist.get_rank(group))
+    return (str(dist.get_backend(group)), ranks)
+
+
 def halo_plan(graph, spec: ShardSpec, group=None) -> "HaloPlan":
-    """The shard's HaloPlan, built once per (graph, destination range, world)
-    and cached on a CSRGraph (a ``(rowptr, col)`` pair: built every call)."""
-    key = (spec.dst_lo, spec.dst_hi, spec.world, spec.rank, id(group))
+    """The shard's HaloPlan, built once per (graph, destination range, world,
+    process group membership) and cached on a CSRGraph (a ``(rowptr, col)``
+    pair: built every call)."""
+    key = (spec.dst_lo, spec.dst_hi, spec.world, spec.rank, _group_key(group))
     cache = getattr(graph, "_halo", None) if hasattr(graph, "_shards") else None
     if cache is not None and key in cache:
         return cache[key]

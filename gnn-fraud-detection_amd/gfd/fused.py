@@ -51,9 +51,14 @@ def bn_affine(bn: Optional[torch.nn.BatchNorm1d], device) -> torch.Tensor:
     return torch.cat([scale, shift]).contiguous()
 
 
-def head_foldable(head, width: int) -> bool:
+def head_foldable(head, width: int, conv=None) -> bool:
     """The model head the store can fold (gfd_epilogue.head_*): Linear(64, 1)
-    in fp32 after a layer whose input width takes the plan-scheduled kernels."""
+    in fp32 after a layer whose input width takes the plan-scheduled kernels
+    (F <= 168) and, when ``conv`` (the last GATConv) is given, whose attention
+    slope those kernels take (leaky01: negative_slope in [0, 1]; others go to
+    the head-less k_fused path, which cannot fold the head -- ADVICE r4)."""
+    if conv is not None and not (0.0 <= float(conv.negative_slope) <= 1.0):
+        return False
     return (head is not None and head.in_features == C and head.out_features == 1 and
             head.weight.dtype == torch.float32 and head.weight.is_cuda and width <= 168 and
             (head.bias is None or head.bias.dtype == torch.float32))
@@ -84,8 +89,9 @@ def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
         res = x if x.dtype == torch.float32 else x.float()
     hout = hw = None
     if head is not None:
-        if not head_foldable(head, F):
-            raise ValueError("gat_layer head: Linear(64, 1) fp32 on the device (head_foldable)")
+        if not head_foldable(head, F, conv):
+            raise ValueError("gat_layer head: Linear(64, 1) fp32 on the device after a layer the "
+                             "plan-scheduled kernels take (head_foldable)")
         hw = head.weight.detach().reshape(-1).contiguous()
         hout = torch.empty((N, 1), dtype=torch.float32, device=dev)
     ep = _lib.GfdEpilogue(ab.data_ptr(), 1 if relu else 0, _lib.ptr(res),

@@ -110,7 +110,7 @@ class GAT(_GATStack):
         if self._fused() and x.is_cuda and self.gat_layers:
             from .fused import head_foldable
             width = self.gat_layers[-1].in_channels
-            if head_foldable(self.out, width):
+            if head_foldable(self.out, width, self.gat_layers[-1]):
                 # inference: Linear(64, 1) folded into the last layer's store
                 # (gat.py:94): the [N, 64] body is never written or re-read
                 return self.encode(x, edge_index, head=self.out)

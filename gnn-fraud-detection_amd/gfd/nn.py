@@ -62,7 +62,9 @@ class GATConvFunction(torch.autograd.Function):
         HC = weight.size(0)
         H, C = SUPPORTED_HEADS, HC // SUPPORTED_HEADS
         plan = graph.plan()
-        need_stats = any(ctx.needs_input_grad[:5])
+        # the softmax statistics only for a backward: not under no_grad (the
+        # module's parameters require grad even in inference)
+        need_stats = torch.is_grad_enabled() and any(ctx.needs_input_grad[:5])
         out = torch.empty((N, C), dtype=torch.float32, device=dev)
         st = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         stats = torch.empty((N, 2 * H), dtype=torch.float32, device=dev) if need_stats else None

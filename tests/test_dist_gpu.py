@@ -154,3 +154,90 @@ def test_rows_copy_gather_scatter(cols, stride):
     assert torch.isnan(dst_base[untouched]).all()
     if stride > cols:
         assert torch.isnan(dst_base[:, :stride - cols]).all()
+
+
+@pytest.mark.parametrize("world,balance", [(2, "messages"), (4, "cost"), (8, "nodes")])
+def test_sharded_train_step_virtual_ranks(world, balance):
+    """The sharded training step (gfd.dist "Sharded training") through the HIP
+    kernels: each virtual rank runs gat_conv_local forward + backward on its
+    LocalGraph (own destinations + halo sources), the ranks' partial parameter
+    gradients are summed (what all_reduce_grads does over RCCL), and the sum
+    must equal the whole-graph gradients; the outputs equal the whole-graph
+    forward's rows.  Each rank's local graph is smaller than the whole graph."""
+    from gfd import dist as gdist, graph as ggraph
+    from gfd.nn import gat_conv
+    dev = torch.device("cuda", 0)
+    N, E, F = 20000, 160000, 166
+    ei, x, W, a_s, a_d, b = _problem(N, E, F, 21, dev)
+    graph = ggraph.csr_from_coo(ei.to(dev), N)
+    xd = x.to(dev)
+    gout = torch.randn(N, C, generator=torch.Generator().manual_seed(3)).to(dev)
+
+    def leaf():
+        return [t.to(dev).clone().requires_grad_(True) for t in (W, a_s, a_d, b)]
+
+    full = leaf()
+    out_full = gat_conv(xd, graph, *full, training=True)
+    (out_full * gout).sum().backward()
+    sh = leaf()
+    spec = gdist.ShardSpec(graph.rowptr, 0, world, balance)
+    outs = []
+    for r in range(world):
+        lo, hi = spec.dst_bounds[r], spec.dst_bounds[r + 1]
+        lg = gdist.local_graph(graph, lo, hi)
+        assert lg.graph.num_nodes < N and lg.n_dst == hi - lo
+        o = gdist.gat_conv_local(xd, lg, *sh, training=True)
+        (o * gout[lo:hi]).sum().backward()      # grads accumulate: the all-reduce's sum
+        outs.append(o.detach())
+    torch.cuda.synchronize()
+    assert_close(torch.cat(outs), out_full.detach(), what=f"sharded outputs, world {world}")
+    for name, a, bb in zip(("W", "att_src", "att_dst", "bias"), sh, full):
+        err = (a.grad - bb.grad).abs().max().item()
+        scale = bb.grad.abs().max().item()
+        assert err <= 1e-4 * scale + 1e-6, f"{name}: {err:.3e} vs scale {scale:.3e} (world {world})"
+
+
+@pytest.mark.parametrize("F,balance", [(64, "cost"), (166, "nodes")])
+def test_halo_tables_never_touch_non_halo_rows(F, balance):
+    """The halo exchange leaves every row outside a shard's own block and its
+    halo unwritten: fill those rows of the exchange tables with
+    NaN -- the [rows, 8] s table and, for a hidden layer, the [rows, 72]
+    h | s table -- and the shard's aggregation through the HIP kernels
+    (light slots' padding, clamped slots, hub chunks) must equal the
+    full-table result bit for bit: no kernel reads a non-halo row."""
+    from gfd import dist as gdist, graph as ggraph
+    from gfd.fused import bn_affine
+    dev = torch.device("cuda", 0)
+    N, E, world = 8000, 64000, 3
+    ei, x, W, a_s, a_d, b = _problem(N, E, F, 17, dev)
+    g = ggraph.csr_from_coo(ei.to(dev), N)
+    W, a_s, a_d, b = W.to(dev), a_s.to(dev), a_d.to(dev), b.to(dev)
+    packed = gdist.pack_weights(W, a_s, a_d)
+    aff = bn_affine(None, dev)
+    h = x.to(dev)
+    st = gdist.logits_rows(h, packed, 0, N)
+    xmax = h.abs().max().reshape(1)
+    for r in range(world):
+        sp = gdist.ShardSpec(g.rowptr, r, world, balance)
+        lo, hi = sp.dst_lo, sp.dst_hi
+        need, _ = gdist.halo_needs(gdist.shard_columns(g, sp), sp)
+        keep = torch.zeros(N, dtype=torch.bool, device=dev)
+        keep[lo:hi] = True
+        keep[need.long()] = True
+        want = gdist.shard_aggregate_ep(h, g, st, packed, b, sp, 0.2, xmax, aff, True, None)
+        # layer 0: x resident, the s table filled only on own + halo rows
+        s_tab = torch.full((N, 8), float("nan"), device=dev)
+        s_tab[keep] = st[keep, :8]
+        got = gdist.shard_aggregate_ep(h, g, gdist.LogitsTable(s_tab, st[lo:hi, 8:]), packed, b,
+                                       sp, 0.2, xmax, aff, True, None)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), f"rank {r}: the s table's non-halo rows were read"
+        if F == 64:   # hidden layer: h and s from one [rows, 72] table
+            tab = torch.full((N, gdist.HID), float("nan"), device=dev)
+            tab[keep, :64] = h[keep]
+            tab[keep, 64:] = st[keep, :8]
+            hv = tab[:, :64]
+            got = gdist.shard_aggregate_ep(hv, g, gdist.LogitsTable(tab[:, 64:], st[lo:hi, 8:]),
+                                           packed, b, sp, 0.2, xmax, aff, True, None)
+            torch.cuda.synchronize()
+            assert torch.equal(got, want), f"rank {r}: the h table's non-halo rows were read"

@@ -202,6 +202,49 @@ def test_backward_heavy_tailed_features(big):
     assert_close_scaled(gb, conv.bias.grad, what="grad_bias")
 
 
+@pytest.mark.parametrize("layout", ["contiguous", "pitch168"])
+def test_forward_logits_heavy_tailed_features(layout):
+    """The logits pass on rows with an outlier feature (its weight zero, so it
+    must not matter): the f16 split under one row scale would lose the row's
+    other features; k_logits_lone detects such rows (nonzero features spanning
+    more than 2^18) and runs their tile on fp32 MFMA.  Checked: the s | t
+    logits (gfd_gat_logits_lone, exact to fp32 against the oracle's) and the
+    self-loop-only rows' outputs, in the inference layout and the reference's
+    contiguous [N, 166] layout."""
+    from gfd import dist as gdist, graph as ggraph, _lib
+    x, ei, conv = _random_case(3000, 9000, 166, seed=33)
+    x[:40, 0] = 1e9 * torch.linspace(-1, 1, 40)
+    with torch.no_grad():
+        conv.lin_src.weight[:, 0] = 0.0
+    N, F = x.shape
+    W = conv.lin_src.weight.detach()
+    h = (x.double() @ W.double().t()).view(N, 8, 64)
+    st_ref = torch.cat([(h * conv.att_src.detach().double()).sum(-1),
+                        (h * conv.att_dst.detach().double()).sum(-1)], 1)
+    if layout == "contiguous":
+        xd = x.to(DEV)
+    else:
+        xd = torch.nn.functional.pad(x, (0, 2)).to(DEV)[:, :F]
+    g = ggraph.csr_from_coo(ei.to(DEV), N)
+    packed = gdist.pack_weights(W.to(DEV), conv.att_src.detach().to(DEV),
+                                conv.att_dst.detach().to(DEV))
+    st = torch.empty((N, 16), device=DEV)
+    out = torch.zeros((N, 64), device=DEV)
+    xmax = torch.zeros(1, device=DEV)
+    _lib.call("gfd_gat_logits_lone", xd.data_ptr(), _lib.x_dtype_code(xd), N, F, xd.stride(0),
+              packed.data_ptr(), 8, 64, g.rowptr.data_ptr(), conv.bias.detach().to(DEV).data_ptr(),
+              0.2, st.data_ptr(), xmax.data_ptr(), out.data_ptr(), None, _lib.stream_handle(DEV))
+    torch.cuda.synchronize()
+    err = (st.cpu().double() - st_ref).abs()
+    bound = 1e-5 * st_ref.abs().amax(1, keepdim=True) + 1e-6
+    assert bool((err <= bound).all()), f"logits: max err {err.max():.3e}"
+    # the self-loop-only rows' outputs (Wbar x_i + bias) on the outlier rows too
+    deg = (g.rowptr[1:] - g.rowptr[:-1]).cpu()
+    lone = torch.nonzero(deg == 1).flatten()
+    ref_out = conv(x, ei).detach()
+    assert_close(out.cpu()[lone], ref_out[lone], what=f"lone rows' outputs ({layout})")
+
+
 def test_backward_heavy_tailed_gradient_rows():
     """A destination whose upstream gradient is 10^6 times the others (hidden
     layer, F = 64: grad_x on the fp16 MFMA path): each dh' row is scaled on its

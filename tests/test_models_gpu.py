@@ -292,3 +292,30 @@ def test_gat_head_folded_into_last_layer_store(layers, F):
         want = body @ m.out.weight.t() + m.out.bias
     assert folded.shape == (N, 1)
     assert_close(folded, want, what=f"folded head, {layers} layers")
+
+
+def test_gat_inference_with_slope_outside_unit_interval():
+    """negative_slope outside [0, 1] takes the k_fused path, which cannot fold
+    the head: GAT.forward must not try and still match the body
+    written out plus the head applied by ATen, and the oracle."""
+    from gfd import synth
+    from gfd.models import GAT
+    from oracle import GATRef
+    torch.manual_seed(12)
+    N, F = 3000, 165
+    ei = torch.from_numpy(synth.power_law(N, 20000, seed=12))
+    x = torch.randn(N, F)
+    ref = GATRef(F, 64, 1, num_layers=2).eval()
+    for conv in ref.gat_layers:
+        conv.negative_slope = 1.5
+    m = GAT(F, 64, 1, num_layers=2).to(DEV).eval()
+    m.load_state_dict(ref.state_dict(), strict=True)
+    for conv in m.gat_layers:
+        conv.negative_slope = 1.5
+    with torch.no_grad():
+        got = m(x.to(DEV), ei.to(DEV))
+        want = ref(x, ei)
+        body = m.encode(x.to(DEV), ei.to(DEV))
+    assert got.shape == (N, 1)
+    assert_close(got, want, what="GAT, slope 1.5")
+    assert_close(got, body @ m.out.weight.t() + m.out.bias, what="GAT, slope 1.5, unfolded head")
