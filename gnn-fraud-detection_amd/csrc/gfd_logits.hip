@@ -207,12 +207,14 @@ k_logits_lone(
 #endif
     // Row conditioning: a row whose smallest nonzero |x| is below 2^-18 of its
     // max has features the one-row-scale f16 split cannot hold to ~2^-21 (an
-    // outlier feature); a tile with such a row runs on fp32 MFMA (wave-uniform)
+    // outlier feature).  A tile with such a row also runs fp32 MFMA, and those
+    // rows (only those: every other row's arithmetic stays its own, whatever
+    // rows share its tile -- shards tile differently) take its results.
     const float rmax_row = max_xor16_32(rm);                 // lanes r, r + 16, r + 32, r + 48
     const float rmin_row = -max_xor16_32(-rmin);
     const bool ill = rin && rmin_row < rmax_row * 0x1p-18f;
     const bool exact = __ballot(ill) != 0;                    // wave-uniform
-    const int er = exact ? 0 : scale_exp(rmax_row);
+    const int er = scale_exp(rmax_row);
     const float rs = ldexpf(1.0f, er);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     f32x4 o[4];
@@ -230,14 +232,46 @@ k_logits_lone(
         return a[2 * tt + (j >> 2)][j & 3];
       }
     };
+#pragma unroll
+    for (int tt = 0; tt < kLKB; ++tt) {
+      if (tt >= KB) break;  // uniform: past the row's k-steps
+      union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x2 v = f32x2{xk(tt, 2 * i), xk(tt, 2 * i + 1)} * f32x2{rs, rs};
+        hi.p[i] = __builtin_convertvector(v, f16x2);
+        lo.u[i] = split_lo(v, hi.u[i]);
+      }
+      {
+        const uint4 uh = UP[0][tt][lane], ul = UP[1][tt][lane];
+        const f16x8 u_h = *reinterpret_cast<const f16x8*>(&uh);
+        const f16x8 u_l = *reinterpret_cast<const f16x8*>(&ul);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_h, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_l, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, u_h, acc, 0, 0, 0);
+      }
+      if (any_lone) {
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
+          const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
+          const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
+          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, o[ct], 0, 0, 0);
+          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, o[ct], 0, 0, 0);
+          o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, o[ct], 0, 0, 0);
+        }
+      }
+    }
+    float ers = ldexpf(1.0f, -er);  // the row's unscale (lanes holding row rl)
     if (exact) {
       // fp32 MFMA 16x16x4: the lane's j-th K value against the fragments'
-      // j-th entry (hi + lo: the packed fp32-faithful value), 8 MFMAs per
-      // f16 k-step and 16-column tile, two accumulator chains each
-      f32x4 acc2 = acc;
-      f32x4 o2[4];
+      // j-th entry (hi + lo: the packed fp32-faithful value), 8 MFMAs per f16
+      // k-step and 16-column tile; then ill rows (result element q of lane
+      // (g, rl) = row 4 g + q) take these sums, unscaled
+      f32x4 ae = {0.f, 0.f, 0.f, 0.f};
+      f32x4 oe[4];
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) o2[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ct = 0; ct < 4; ++ct) oe[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int tt = 0; tt < kLKB; ++tt) {
         if (tt >= KB) break;  // uniform: past the row's k-steps
@@ -245,11 +279,9 @@ k_logits_lone(
         const f16x8 u_h = *reinterpret_cast<const f16x8*>(&uh);
         const f16x8 u_l = *reinterpret_cast<const f16x8*>(&ul);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          f32x4& ac = (j & 1) ? acc2 : acc;
-          ac = __builtin_amdgcn_mfma_f32_16x16x4f32(xk(tt, j), float(u_h[j]) + float(u_l[j]), ac,
+        for (int j = 0; j < 8; ++j)
+          ae = __builtin_amdgcn_mfma_f32_16x16x4f32(xk(tt, j), float(u_h[j]) + float(u_l[j]), ae,
                                                    0, 0, 0);
-        }
         if (any_lone) {
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct) {
@@ -257,48 +289,22 @@ k_logits_lone(
             const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
             const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              f32x4& oc = (j & 1) ? o2[ct] : o[ct];
-              oc = __builtin_amdgcn_mfma_f32_16x16x4f32(xk(tt, j), float(b_h[j]) + float(b_l[j]),
-                                                       oc, 0, 0, 0);
-            }
+            for (int j = 0; j < 8; ++j)
+              oe[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                  xk(tt, j), float(b_h[j]) + float(b_l[j]), oe[ct], 0, 0, 0);
           }
         }
       }
-      acc += acc2;
+      const int ill_i = ill ? 1 : 0;
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) o[ct] += o2[ct];
-    } else {
+      for (int q = 0; q < 4; ++q) {
+        if (__builtin_amdgcn_ds_bpermute((4 * g + q) << 2, ill_i)) {
+          acc[q] = ae[q];
 #pragma unroll
-      for (int tt = 0; tt < kLKB; ++tt) {
-        if (tt >= KB) break;  // uniform: past the row's k-steps
-        union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } hi, lo;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const f32x2 v = f32x2{xk(tt, 2 * i), xk(tt, 2 * i + 1)} * f32x2{rs, rs};
-          hi.p[i] = __builtin_convertvector(v, f16x2);
-          lo.u[i] = split_lo(v, hi.u[i]);
-        }
-        {
-          const uint4 uh = UP[0][tt][lane], ul = UP[1][tt][lane];
-          const f16x8 u_h = *reinterpret_cast<const f16x8*>(&uh);
-          const f16x8 u_l = *reinterpret_cast<const f16x8*>(&ul);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_h, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, u_l, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, u_h, acc, 0, 0, 0);
-        }
-        if (any_lone) {
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) {
-            const uint4 bh = WB[0][tt][ct][lane], bl = WB[1][tt][ct][lane];
-            const f16x8 b_h = *reinterpret_cast<const f16x8*>(&bh);
-            const f16x8 b_l = *reinterpret_cast<const f16x8*>(&bl);
-            o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_h, o[ct], 0, 0, 0);
-            o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi.v, b_l, o[ct], 0, 0, 0);
-            o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo.v, b_h, o[ct], 0, 0, 0);
-          }
+          for (int ct = 0; ct < 4; ++ct) o[ct][q] = oe[ct][q];
         }
       }
+      if (ill) ers = 1.0f;
     }
     // acc / o[ct] element q of lane l: row 4 g + q, column rl (16 ct + rl);
     // the row's unscale comes from a lane holding that row.  (Lane-derived
@@ -307,7 +313,6 @@ k_logits_lone(
     lane = opaque(lane0);
     rl = lane & 15;
     g = lane >> 4;
-    const float ers = ldexpf(1.0f, -er);
     float sv[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {

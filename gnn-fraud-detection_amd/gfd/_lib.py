@@ -55,6 +55,7 @@ PLAN = ct.POINTER(GfdPlan)
 SIGNATURES = {
     "gfd_status_string": (ct.c_char_p, [c_i32]),
     "gfd_abi_version": (ct.c_int, []),
+    "gfd_build_id": (ct.c_char_p, []),
     "gfd_csr_workspace_size": (c_sz, [c_i64, c_i64]),
     "gfd_csr_from_coo": (c_i32, [P, c_i64, c_i64, P, P, P, c_sz, P]),
     "gfd_coo_fingerprint": (c_i32, [P, c_i64, P, P]),

@@ -47,7 +47,7 @@ class GATConvFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, att_src, att_dst, bias, graph: CSRGraph, negative_slope: float,
-                dropout_p: float, seed: int):
+                dropout_p: float, seed: int, grad_mode: bool = True):
         dev = x.device
         _check_tensor("x", x, dev, (torch.float32, torch.bfloat16))
         for n, t in (("weight", weight), ("att_src", att_src), ("att_dst", att_dst)):
@@ -63,8 +63,9 @@ class GATConvFunction(torch.autograd.Function):
         H, C = SUPPORTED_HEADS, HC // SUPPORTED_HEADS
         plan = graph.plan()
         # the softmax statistics only for a backward: not under no_grad (the
-        # module's parameters require grad even in inference)
-        need_stats = torch.is_grad_enabled() and any(ctx.needs_input_grad[:5])
+        # module's parameters require grad even in inference; grad_mode is the
+        # caller's torch.is_grad_enabled(), which is off inside forward)
+        need_stats = grad_mode and any(ctx.needs_input_grad[:5])
         out = torch.empty((N, C), dtype=torch.float32, device=dev)
         st = torch.empty((N, 2 * H), dtype=torch.float32, device=dev)
         stats = torch.empty((N, 2 * H), dtype=torch.float32, device=dev) if need_stats else None
@@ -113,7 +114,7 @@ class GATConvFunction(torch.autograd.Function):
                   _lib.stream_handle(dev))
         if gx is not None and x.dtype != torch.float32:
             gx = gx.to(x.dtype)
-        return gx, gw, gas, gad, gb, None, None, None, None
+        return gx, gw, gas, gad, gb, None, None, None, None, None
 
 
 def gat_conv(x: torch.Tensor, edge_index_or_graph, weight: torch.Tensor, att_src: torch.Tensor,
@@ -128,7 +129,7 @@ def gat_conv(x: torch.Tensor, edge_index_or_graph, weight: torch.Tensor, att_src
     dp = float(dropout) if training else 0.0
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if dp > 0 else 0
     return GATConvFunction.apply(x, weight, att_src.reshape(-1), att_dst.reshape(-1), bias,
-                                 graph, negative_slope, dp, seed)
+                                 graph, negative_slope, dp, seed, torch.is_grad_enabled())
 
 
 def _glorot(t: torch.Tensor):

@@ -47,8 +47,18 @@ def test_ctypes_table_matches_header(lib):
         assert len(params) == len(args), f"{name}: header has {len(params)} params, ctypes {len(args)}"
 
 
+def test_build_id_is_the_source_hash(lib):
+    """Provenance: the loaded library carries the SHA-256 of the sources,
+    headers and flags it was built from, and it is this tree's."""
+    from gfd import build
+    got = lib.gfd_build_id().decode()
+    assert got.startswith(build.ID_TAG + build.source_id(build.BASE_FLAGS)), got
+    assert build.library_id(build.lib_path()) == build.source_id(build.BASE_FLAGS)
+    assert not build.needs_build(build.lib_path(), build.BASE_FLAGS)
+
+
 def test_version_and_status_strings(lib):
-    assert lib.gfd_abi_version() == 4
+    assert lib.gfd_abi_version() == 5
     assert b"range" in lib.gfd_status_string(2)
     assert lib.gfd_status_string(99) == b"unknown status"
 
