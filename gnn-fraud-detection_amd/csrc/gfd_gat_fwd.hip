@@ -86,12 +86,13 @@ gfd_status tiles_impl(const AggArgs& a, const PackLayout& L, hipStream_t stream)
   if (!p.class_split) return GFD_OK;  // the general kernel took every tile
   // lone slots need 16-B aligned rows and no dropout (k_lone projects with the
   // head mean; a dropout mask differs per head); otherwise the light kernel
-  // runs to the end and takes them as one-message slots
+  // runs to the end and takes them as one-message slots -- unless the lone
+  // class is not asked for (the logits pass produced it: gfd_gat_fwd_ep)
   const uintptr_t base = reinterpret_cast<uintptr_t>(a.x);
   const int eb = a.xdt == GFD_DTYPE_BF16 ? 2 : 4;
   const bool lone = base % 16 == 0 && (a.ldx * eb) % 16 == 0 && L.KB <= 6 && a.dp == 0.f;
   if (cls & kLightBit) {
-    const gfd_status s = launch_light(a, L, !lone, stream);
+    const gfd_status s = launch_light(a, L, !lone && (cls & kLoneBit), stream);
     if (s != GFD_OK) return s;  // the class split promised a light kernel for this F
   }
   return (lone && (cls & kLoneBit)) ? launch_lone(a, L, stream) : GFD_OK;

@@ -262,7 +262,8 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int in_fea
 #define GFD_STAGE_ALL 3
 /* single tile classes (profiling splits; the union equals GFD_STAGE_TILES):
  * general (k_stream<general>, or k_fused for F > 168), light
- * (k_stream<light>), lone (k_lone) */
+ * (k_stream<light>), lone (k_lone; for rows that are not 16-B aligned the light
+ * kernel takes the lone class, when GFD_STAGE_TILES_LONE is asked for) */
 #define GFD_STAGE_TILES_GENERAL 4
 #define GFD_STAGE_TILES_LIGHT 8
 #define GFD_STAGE_TILES_LONE 16
