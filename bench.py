@@ -715,7 +715,7 @@ def main():
             legs["c4_layer_fwd_bwd_dropout"] = bench_legs.c4_layer_fwd_bwd(s, dev, dropout=0.2)
         if "dropin" in want:
             log("[bench] leg drop-in module (gfd.nn.GATConv on the COO edge_index) ...")
-            legs["c4_dropin_module"] = bench_legs.dropin_module(s, dev, res["ms_per_step"])
+            legs["c4_dropin_module"] = bench_legs.dropin_module(s, dev, res.get("ms_per_step"))
         if "sample" in want:
             log("[bench] leg neighbour sampling on the C4 graph ...")
             legs["neighbor_sampling"] = bench_legs.neighbor_sampling(s, dev)

@@ -338,7 +338,7 @@ def dropin_module(s, dev, headline_ms, steps=10, warmup=2):
         res[name] = {"ms_per_step": med, "ms_mean": mean,
                      "value": g.num_input_edges / (med * 1e-3),
                      "row_pitch_bytes": x.stride(0) * x.element_size(),
-                     "vs_headline": headline_ms / med}
+                     "vs_headline": headline_ms / med if headline_ms else None}
         del x, out
         torch.cuda.empty_cache()
     res["graph_lookups"] = {k: ggraph.STATS[k] - lookups0[k] for k in ggraph.STATS}
