@@ -18,7 +18,7 @@ for a in "$@"; do
   python3 - "$a" gpurun_out/${TAG}_b$i.json <<'PY'
 import json, sys
 d = json.load(open(sys.argv[2]))
-print(f"[{sys.argv[1]}]", round(d["ms_per_step"], 3), {k: round(x["ms"], 3) for k, x in d["kernels"].items()})
+print(f"[{sys.argv[1]}]", round(d.get("ms_per_step", 0), 3), {k: round(x["ms"], 3) for k, x in d.get("kernels", {}).items()})
 for name, leg in d.get("legs", {}).items():
     print("  leg", name, json.dumps({k: v for k, v in leg.items() if k in ("ms_per_step", "forward_ms", "backward_ms", "contiguous_166", "pitch_168_view", "max_grad_err_over_tolerance")}))
 PY
