@@ -31,6 +31,11 @@
 //   k_colsum64    grad_bias = column sums of g (fixed-grid partials)
 //   k_gx / k_gemm grad_x = dh W (only when requested; f16 MFMA for F <= 64)
 // Deterministic: no float atomics anywhere; every sum has a fixed order.
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+
 #include "gfd_check.h"
 #include "gfd_fwd.h"
 
@@ -1090,7 +1095,7 @@ struct FLay {
   int yt, hp, ahi, alo, bhi, blo, ysc, yinv, iax, csb, dtt, pw, cw, hpr, bytes;
 };
 
-__host__ __device__ inline FLay flay(int Fu) {
+__host__ __device__ inline FLay flay(int Fu, int NW) {
   FLay L;
   int o = 0;
   auto take = [&o](int bytes) {
@@ -1099,7 +1104,7 @@ __host__ __device__ inline FLay flay(int Fu) {
     return r;
   };
   L.yt = take(kFK * kFYP * 4);
-  L.hp = take(8 * kFYP * 4);
+  L.hp = take(NW * kFYP * 4);
   L.ahi = take(kFR * kGPt * 2);
   L.alo = take(kFR * kGPt * 2);
   L.bhi = take(Fu * kGPt * 2);
@@ -1109,9 +1114,9 @@ __host__ __device__ inline FLay flay(int Fu) {
   L.iax = take(16 * 4);
   L.csb = take(kGMaxF * 4);
   L.dtt = take(kFK * 8 * 4);
-  L.pw = take(2 * 8 * 33 * 4);  // per tile parity, per wave
-  L.cw = take(2 * 8 * 32 * 4);
-  L.hpr = take(8 * 4);
+  L.pw = take(2 * NW * 33 * 4);  // per tile parity, per wave
+  L.cw = take(2 * NW * 32 * 4);
+  L.hpr = take(NW * 4);
   L.bytes = o;
   return L;
 }
@@ -1125,8 +1130,8 @@ __host__ __device__ inline FLay flay(int Fu) {
 __device__ unsigned long long g_fprof[10];
 #endif
 
-template <typename XT, bool VEC, int NJ>
-__global__ void __launch_bounds__(512) k_src_gw(
+template <typename XT, bool VEC, int NJ, int NW>
+__global__ void __launch_bounds__(64 * NW) k_src_gw(
     const int32_t* __restrict__ colptr, const int32_t* __restrict__ csc_dst,
     const int32_t* __restrict__ csc_eid, const int32_t* __restrict__ src_hub_rank,
     const float* __restrict__ dhub, const float* __restrict__ rec, const float* __restrict__ dt,
@@ -1134,7 +1139,20 @@ __global__ void __launch_bounds__(512) k_src_gw(
     int F, int Fu, const int32_t* __restrict__ bounds, int S, const uint32_t* __restrict__ amax,
     float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) char fsm[];
-  const FLay L = flay(Fu);
+  // NW = 8 or 16 waves: a wave walks 1 / NW of a tile's messages and holds
+  // 1 / NW of the accumulator (n-tiles wn + (NW / 4) j)
+  static_assert(NW == 8 || NW == 16, "k_src_gw: 8 or 16 waves");
+  constexpr int NPW = kFK / NW;            // nodes per wave (dt, hub / zero rows)
+  constexpr int NB = NW == 8 ? kFNB : 2;   // batches of 8 messages per chunk
+  constexpr int NCH = 8 * NB;              // messages per chunk
+  constexpr int NTH = 64 * NW;             // threads
+  constexpr int XIT = 1024 / NTH;          // x-tile items per thread
+  constexpr int WN = NW / 4;               // n-tile stride
+  constexpr int NX = (12 + NW - 1) / NW;   // ds / dt n-tiles per wave
+  constexpr int LGW = NW == 8 ? 3 : 4;
+  constexpr int TPC = NTH / 256;           // column-pass threads per y column
+  constexpr int NPT = kFK / TPC;           // nodes per column-pass thread
+  const FLay L = flay(Fu, NW);
   float* yt = reinterpret_cast<float*>(fsm + L.yt);
   float* hp = reinterpret_cast<float*>(fsm + L.hp);
   _Float16* Ahi = reinterpret_cast<_Float16*>(fsm + L.ahi);
@@ -1169,7 +1187,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
   }
   if (tid < kGMaxF)
     csb[tid] = tid < F ? ldexpf(1.0f, scale_exp(__uint_as_float(amax[kDH + tid]))) : 1.0f;
-  for (int i = tid; i < (kFR - kFE) * kGPt; i += 512) {
+  for (int i = tid; i < (kFR - kFE) * kGPt; i += NTH) {
     Ahi[kFE * kGPt + i] = _Float16(0.f);
     Alo[kFE * kGPt + i] = _Float16(0.f);
   }
@@ -1178,8 +1196,8 @@ __global__ void __launch_bounds__(512) k_src_gw(
 
   // this wave's copies of a tile's message prefix and its sources' CSC starts,
   // by tile parity (tile t + 1's are written during tile t's walk)
-  auto Pof = [&](int par) { return pw + (par * 8 + wave) * 33; };
-  auto Cof = [&](int par) { return cw + (par * 8 + wave) * 32; };
+  auto Pof = [&](int par) { return pw + (par * NW + wave) * 33; };
+  auto Cof = [&](int par) { return cw + (par * NW + wave) * 32; };
   // largest r in [0, 32) with P[r] <= f (P non-decreasing; f < P[32])
   auto find = [](const int* P, int f) {
     int r = 0;
@@ -1191,7 +1209,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
 
   // --- per-wave pipeline state ---
   int n_c0 = 0, n_c1 = 0, n_hr = -1;  // tile t + 2 (loaded during t): lane r's colptr pair, hub rank
-  float n_dt = 0.f;                   // tile t + 1: dt of node 4 wave + (lane >> 3), head lane & 7
+  float n_dt = 0.f;                   // tile t + 1: dt of node NPW wave + (lane >> 3), head lane & 7
   // tile t's walk state (code: lane r's hub rank | -1 | -2 outside | -3 no messages;
   // [lo, hi): the wave's message range, rfirst its first source, head: begun by an
   // earlier wave) and tile t + 1's, prepared during tile t's walk (x_)
@@ -1199,9 +1217,9 @@ __global__ void __launch_bounds__(512) k_src_gw(
   bool head = false;
   int x_code = -2, x_lo = 0, x_hi = 0, x_rf = 0;
   bool x_head = false;
-  int pe[kFNB], pi[kFNB], rr[kFNB];       // chunk: edge ids, destinations, source per slot
-  int x_pe[kFNB], x_pi[kFNB], x_rr[kFNB];  // tile t + 1's first chunk
-  float pa[kFNB], pd[kFNB], pg[kFNB][8];  // chunk: alpha~, dpre (lane 8 slot + head), g rows
+  int pe[NB], pi[NB], rr[NB];       // chunk: edge ids, destinations, source per slot
+  int x_pe[NB], x_pi[NB], x_rr[NB];  // tile t + 1's first chunk
+  float pa[NB], pd[NB], pg[NB][8];  // chunk: alpha~, dpre (lane 8 slot + head), g rows
 
   auto load_next = [&](int64_t k0) {
     const int64_t j = k0 + (lane & 31);
@@ -1211,13 +1229,13 @@ __global__ void __launch_bounds__(512) k_src_gw(
     if (src_hub_rank) n_hr = src_hub_rank[jc];
   };
   auto load_dt = [&](int64_t k0) {
-    const int64_t jd = k0 + 4 * wave + ((lane >> 3) & 3);
+    const int64_t jd = k0 + NPW * wave + ((lane >> 3) & (NPW - 1));
     n_dt = dt[(jd < ke ? jd : kb) * 8 + (lane & 7)];
   };
-  auto issue_idx = [&](const int* P, const int* Cs, int c, int h_end, int (&e_)[kFNB],
-                       int (&i_)[kFNB], int (&r_)[kFNB]) {
+  auto issue_idx = [&](const int* P, const int* Cs, int c, int h_end, int (&e_)[NB],
+                       int (&i_)[NB], int (&r_)[NB]) {
 #pragma unroll
-    for (int bb = 0; bb < kFNB; ++bb) {
+    for (int bb = 0; bb < NB; ++bb) {
       const int f = c + 8 * bb + (lane >> 3);
       const bool ok = f < h_end;
       const int r = find(P, ok ? f : c);
@@ -1232,7 +1250,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
     return;
 #endif
 #pragma unroll
-    for (int bb = 0; bb < kFNB; ++bb) {
+    for (int bb = 0; bb < NB; ++bb) {
       const float* rp = rec + int64_t(pe[bb]) * kRec + (lane & 7);
       pa[bb] = rp[0];
       pd[bb] = rp[H];
@@ -1267,8 +1285,8 @@ __global__ void __launch_bounds__(512) k_src_gw(
       Cs[lane] = n_c0;
     }
     if (lane == 0) P[32] = D;
-    x_lo = int((int64_t(wave) * D) >> 3);
-    x_hi = int((int64_t(wave + 1) * D) >> 3);
+    x_lo = int((int64_t(wave) * D) >> LGW);
+    x_hi = int((int64_t(wave + 1) * D) >> LGW);
     if (x_lo < x_hi) {
       x_rf = __builtin_amdgcn_readfirstlane(find(P, x_lo));
       x_head = x_lo > P[x_rf];
@@ -1284,7 +1302,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
     rfirst = x_rf;
     head = x_head;
 #pragma unroll
-    for (int bb = 0; bb < kFNB; ++bb) {
+    for (int bb = 0; bb < NB; ++bb) {
       pe[bb] = x_pe[bb];
       pi[bb] = x_pi[bb];
       rr[bb] = x_rr[bb];
@@ -1304,7 +1322,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
   auto chunk_ds = [&]() {
     float d = 0.f;
 #pragma unroll
-    for (int bb = 0; bb < kFNB; ++bb) d += sum_xor8_16_32(rr[bb] == cur ? pd[bb] : 0.f);
+    for (int bb = 0; bb < NB; ++bb) d += sum_xor8_16_32(rr[bb] == cur ? pd[bb] : 0.f);
     return d;
   };
   auto flush = [&]() {
@@ -1319,7 +1337,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
   };
   auto consume = [&](int n) {
 #pragma unroll
-    for (int k = 0; k < kFCh; ++k) {
+    for (int k = 0; k < NCH; ++k) {
       if (k < n) {
         const int bb = k >> 3, kk = k & 7;
         const int rk = __builtin_amdgcn_readlane(rr[bb], 8 * kk);
@@ -1344,8 +1362,8 @@ __global__ void __launch_bounds__(512) k_src_gw(
   auto hub_rows = [&]() {
     const int ln = opaque(lane);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = 4 * wave + q;
+    for (int q = 0; q < NPW; ++q) {
+      const int r = NPW * wave + q;
       const int cd = __builtin_amdgcn_readlane(code, r);
       if (cd >= 0) {
         const float* src = dhub + int64_t(cd) * kDH;
@@ -1362,11 +1380,11 @@ __global__ void __launch_bounds__(512) k_src_gw(
   };
 
   // x tile: 2 items x 2 nodes x 4 columns per thread (k_gw's B staging)
-  f32x4 xs[2][2];
+  f32x4 xs[XIT][2];
   auto load_x = [&](int64_t k0, int tq) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int i = tq + 512 * it, p = i & 15, c = i >> 4;
+    for (int it = 0; it < XIT; ++it) {
+      const int i = tq + NTH * it, p = i & 15, c = i >> 4;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int64_t r = k0 + 2 * p + e;
@@ -1379,8 +1397,8 @@ __global__ void __launch_bounds__(512) k_src_gw(
     uint32_t* bh = reinterpret_cast<uint32_t*>(Bhi);
     uint32_t* bl = reinterpret_cast<uint32_t*>(Blo);
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int i = tq + 512 * it, p = i & 15, c = i >> 4;
+    for (int it = 0; it < XIT; ++it) {
+      const int i = tq + NTH * it, p = i & 15, c = i >> 4;
       if (i < nB) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1393,43 +1411,44 @@ __global__ void __launch_bounds__(512) k_src_gw(
       }
     }
   };
-  // 16 values of A row m (nodes 16 kh ..) scaled by sc -> f16 hi / lo image
-  auto put_row = [&](int m, int kh, const float (&v)[16], float sc) {
-    uint32_t hv[8], lv[8];
+  // NPT values of A row m (nodes NPT kh ..) scaled by sc -> f16 hi / lo image
+  auto put_row = [&](int m, int kh, const float (&v)[NPT], float sc) {
+    uint32_t hv[NPT / 2], lv[NPT / 2];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) hv[p] = pk_hi_lo(v[2 * p] * sc, v[2 * p + 1] * sc, lv[p]);
-    uint4* ah = reinterpret_cast<uint4*>(Ahi + m * kGPt + 16 * kh);
-    uint4* al = reinterpret_cast<uint4*>(Alo + m * kGPt + 16 * kh);
-    ah[0] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
-    ah[1] = make_uint4(hv[4], hv[5], hv[6], hv[7]);
-    al[0] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
-    al[1] = make_uint4(lv[4], lv[5], lv[6], lv[7]);
+    for (int p = 0; p < NPT / 2; ++p) hv[p] = pk_hi_lo(v[2 * p] * sc, v[2 * p + 1] * sc, lv[p]);
+    uint4* ah = reinterpret_cast<uint4*>(Ahi + m * kGPt + NPT * kh);
+    uint4* al = reinterpret_cast<uint4*>(Alo + m * kGPt + NPT * kh);
+#pragma unroll
+    for (int u = 0; u < NPT / 8; ++u) {
+      ah[u] = make_uint4(hv[4 * u], hv[4 * u + 1], hv[4 * u + 2], hv[4 * u + 3]);
+      al[u] = make_uint4(lv[4 * u], lv[4 * u + 1], lv[4 * u + 2], lv[4 * u + 3]);
+    }
   };
-  // y column m (< 256) over nodes 16 kh .. 16 kh + 15 (partials merged; rows of
-  // sources without messages hold the hub row or zeros)
+  // y column m (< 256) over nodes NPT kh .. NPT kh + NPT - 1 (partials merged;
+  // rows of sources without messages hold the hub row or zeros)
   // hw[w]: the source of wave w's head-partial row (-1: none), wave order
-  auto ycolumn = [&](int m, int kh, const int (&hw)[8]) {
+  auto ycolumn = [&](int m, int kh, const int (&hw)[NW]) {
     // the partials of this thread's nodes first, in wave order (a fixed order;
     // the same thread reads the sums back: no barrier)
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const int r = hw[w];
-      if (r >= 16 * kh && r < 16 * kh + 16) yt[r * kFYP + m] += hp[w * kFYP + m];
+      if (r >= NPT * kh && r < NPT * kh + NPT) yt[r * kFYP + m] += hp[w * kFYP + m];
     }
-    float v[16];
+    float v[NPT];
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) v[kk] = yt[(16 * kh + kk) * kFYP + m];
+    for (int kk = 0; kk < NPT; ++kk) v[kk] = yt[(NPT * kh + kk) * kFYP + m];
     put_row(m, kh, v, ysc[m & 63]);
   };
   // ds (half 0) / dt (half 1) column e (one per wave): lane k < 32 holds node k's
   // value; the tile's exact max scales it
-  auto xcolumn = [&](int e, const int (&hw)[8]) {
+  auto xcolumn = [&](int e, const int (&hw)[NW]) {
     const int ln = opaque(lane);
     const int k = ln & 31;
     float val = half ? dtt[k * 8 + e] : yt[k * kFYP + 256 + e];
     if (!half) {  // ds partials of node k, in wave order
 #pragma unroll
-      for (int w = 0; w < 8; ++w)
+      for (int w = 0; w < NW; ++w)
         if (hw[w] == k) val += hp[w * kFYP + 256 + e];
     }
     if (ln >= 32) val = 0.f;
@@ -1443,15 +1462,35 @@ __global__ void __launch_bounds__(512) k_src_gw(
     if (ln == 0) iax[e] = ldexpf(1.0f, -ex);
   };
 
-  f32x4 acc[4][NJ], accx[2];
+  f32x4 acc[4][NJ], accx[NX];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  accx[0] = accx[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j2 = 0; j2 < NX; ++j2) accx[j2] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mfma_tile = [&]() {
     const int ln = opaque(lane);
     const int fo = (ln & 15) * kGPt + 8 * (ln >> 4);
+    if constexpr (NW == 16) {  // register-lean order: one m-tile's A at a time
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mt = wm + 4 * i;
+        const f16x8 a_h = *reinterpret_cast<const f16x8*>(Ahi + mt * 16 * kGPt + fo);
+        const f16x8 a_l = *reinterpret_cast<const f16x8*>(Alo + mt * 16 * kGPt + fo);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int nt = wn + WN * j;
+          if (nt < NTn) {
+            const f16x8 b_hi = *reinterpret_cast<const f16x8*>(Bhi + nt * 16 * kGPt + fo);
+            const f16x8 b_lo = *reinterpret_cast<const f16x8*>(Blo + nt * 16 * kGPt + fo);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, b_hi, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, b_lo, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l, b_hi, acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    } else {
     f16x8 a_hi[4], a_lo[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1461,7 +1500,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int nt = wn + 2 * j;
+      const int nt = wn + WN * j;
       if (nt < NTn) {
         const f16x8 b_hi = *reinterpret_cast<const f16x8*>(Bhi + nt * 16 * kGPt + fo);
         const f16x8 b_lo = *reinterpret_cast<const f16x8*>(Blo + nt * 16 * kGPt + fo);
@@ -1473,12 +1512,13 @@ __global__ void __launch_bounds__(512) k_src_gw(
         }
       }
     }
+    }
     const f16x8 x_hi = *reinterpret_cast<const f16x8*>(Ahi + 16 * 16 * kGPt + fo);
     const f16x8 x_lo = *reinterpret_cast<const f16x8*>(Alo + 16 * 16 * kGPt + fo);
     const f32x4 xsc = *reinterpret_cast<const f32x4*>(iax + 4 * (ln >> 4));
 #pragma unroll
-    for (int j2 = 0; j2 < 2; ++j2) {
-      const int nt = wave + 8 * j2;
+    for (int j2 = 0; j2 < NX; ++j2) {
+      const int nt = wave + NW * j2;
       if (nt < NTn) {
         const f16x8 b_hi = *reinterpret_cast<const f16x8*>(Bhi + nt * 16 * kGPt + fo);
         const f16x8 b_lo = *reinterpret_cast<const f16x8*>(Blo + nt * 16 * kGPt + fo);
@@ -1522,9 +1562,9 @@ __global__ void __launch_bounds__(512) k_src_gw(
     if (t > 0) mfma_tile();
 #endif
     GFD_FSTAMP(0);
-    if (lane < 32)
-      dtt[(4 * wave + (lane >> 3)) * 8 + (lane & 7)] =
-          k0 + 4 * wave + (lane >> 3) < ke ? n_dt : 0.f;
+    if (lane < 8 * NPW)
+      dtt[(NPW * wave + (lane >> 3)) * 8 + (lane & 7)] =
+          k0 + NPW * wave + (lane >> 3) < ke ? n_dt : 0.f;
     if (t + 1 < T) {
       prep(k0 + kFK, int(t + 1) & 1);  // tile t + 1's first-chunk indices fly during this walk
       load_dt(k0 + kFK);
@@ -1543,16 +1583,16 @@ __global__ void __launch_bounds__(512) k_src_gw(
 #pragma unroll
       for (int hl = 0; hl < 4; ++hl) y[hl] = 0.f;
       ds = 0.f;
-      consume(min(hi - lo, kFCh));
+      consume(min(hi - lo, NCH));
 #ifdef GFD_AB_F_NOEXTRA  // ablation: first chunk only (wrong sums for long ranges)
-      for (int c = hi; c < hi; c += kFCh) {
+      for (int c = hi; c < hi; c += NCH) {
 #else
-      for (int c = lo + kFCh; c < hi; c += kFCh) {  // long ranges: further chunks in place
+      for (int c = lo + NCH; c < hi; c += NCH) {  // long ranges: further chunks in place
 #endif
         if (half == 0) ds += chunk_ds();  // the running source's ds from this chunk
         issue_idx(Pof(int(t) & 1), Cof(int(t) & 1), c, hi, pe, pi, rr);
         issue_data();
-        consume(min(hi - c, kFCh));
+        consume(min(hi - c, NCH));
       }
       flush();
     }
@@ -1574,12 +1614,12 @@ __global__ void __launch_bounds__(512) k_src_gw(
     // ---- column pass (head partials merged by the threads that read them) ----
     {
       const int tq = opaque(tid);
-      int hw[8];
+      int hw[NW];
 #pragma unroll
-      for (int w = 0; w < 8; ++w) hw[w] = __builtin_amdgcn_readfirstlane(hpr[w]);
+      for (int w = 0; w < NW; ++w) hw[w] = __builtin_amdgcn_readfirstlane(hpr[w]);
 #ifndef GFD_AB_F_NOCOL
-      ycolumn(tq >> 1, tq & 1, hw);
-      xcolumn(wave, hw);
+      ycolumn(tq / TPC, tq % TPC, hw);
+      if (wave < 8) xcolumn(wave, hw);
 #endif
     }
     __syncthreads();
@@ -1603,7 +1643,7 @@ __global__ void __launch_bounds__(512) k_src_gw(
     const int mt = wm + 4 * i;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int nt = wn + 2 * j;
+      const int nt = wn + WN * j;
       const int n = nt * 16 + (lane & 15);
       if (nt >= NTn || n >= F) continue;
       const float ub = 1.0f / csb[n];  // exact: powers of two, undone in two steps
@@ -1615,8 +1655,8 @@ __global__ void __launch_bounds__(512) k_src_gw(
     }
   }
 #pragma unroll
-  for (int j2 = 0; j2 < 2; ++j2) {
-    const int nt = wave + 8 * j2;
+  for (int j2 = 0; j2 < NX; ++j2) {
+    const int nt = wave + NW * j2;
     const int n = nt * 16 + (lane & 15);
     if (nt >= NTn || n >= F) continue;
     const float ub = 1.0f / csb[n];
@@ -2016,6 +2056,7 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
 // hub rows in the dh region, which the fused pass does not otherwise use.
 struct FusedPlan {
   int S = 0;  // 0: unfused
+  int NW = 8;  // waves per block (GFD_BWD_FUSED=1: 8, =2: 16)
   int64_t nt = 0;
   size_t scratch = 0, pre_off = 0, bounds_off = 0;
 };
@@ -2023,7 +2064,8 @@ struct FusedPlan {
 FusedPlan fused_plan(int64_t N, int F, int64_t shubs, bool want_gx) {
   FusedPlan p;
   const char* e = getenv("GFD_BWD_FUSED");
-  if (want_gx || !(e && e[0] == '1') || (F + 15) / 16 * 16 > kFMaxFu) return p;
+  if (want_gx || !(e && (e[0] == '1' || e[0] == '2')) || (F + 15) / 16 * 16 > kFMaxFu) return p;
+  p.NW = e[0] == '2' ? 16 : 8;
   int64_t S = (N + 4095) / 4096;
   if (S > cu_count()) S = cu_count();
   if (S < 1) S = 1;
@@ -2033,7 +2075,7 @@ FusedPlan fused_plan(int64_t N, int F, int64_t shubs, bool want_gx) {
   p.bounds_off = p.pre_off + align_up(sizeof(int64_t) * size_t(p.nt + 1), 256);
   const size_t need = p.scratch + p.bounds_off + sizeof(int32_t) * size_t(S + 1);
   if (need > sizeof(float) * size_t(N) * kDH) return p;  // no room: unfused
-  if (size_t(flay((F + 15) / 16 * 16).bytes) > 160 * 1024) return p;
+  if (size_t(flay((F + 15) / 16 * 16, p.NW).bytes) > 160 * 1024) return p;
   p.S = int(S);
   return p;
 }
@@ -2094,6 +2136,40 @@ gfd_status launch_msg_x(int KF, const void* x, int F, int Fu, int64_t ldx, const
 #undef GFD_MSG
 }
 
+// A non-blocking side stream per device for the passes that need neither the
+// destination pass nor the source pass (k_xmax: x only; k_colsum64: g only).
+// They fork from the caller's stream after the amax reset and join it before
+// the source pass, running beside k_bwd_msg -- whose one block per CU leaves
+// HBM bandwidth idle during its U phase.  The fork / join enqueue sequence of
+// one call holds the device's lock (it never waits on the device); under
+// stream capture the fork is captured as a cross-stream dependency.
+// GFD_BWD_SIDE=0: everything on the caller's stream (A/B).
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
+};
+
+SideStream* side_stream() {
+  const char* e = getenv("GFD_BWD_SIDE");
+  if (e && e[0] == '0') return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<SideStream>> per_dev;
+  std::lock_guard<std::mutex> g(mu);
+  std::unique_ptr<SideStream>& p = per_dev[dev];
+  if (!p) {
+    std::unique_ptr<SideStream> n(new SideStream);
+    if (hipStreamCreateWithFlags(&n->s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&n->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&n->join, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+    p = std::move(n);
+  }
+  return p.get();
+}
+
 template <typename XT>
 gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
                     const int32_t* col, const gfd_plan* plan, const int32_t* colptr,
@@ -2133,25 +2209,46 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   const int64_t nfr = int64_t(H) * 2 * NT * 64;
   k_bwd_wpack<<<unsigned((nfr + 255) / 256), 256, 0, stream>>>(W, F, NT, whdr, bhi, blo);
   GFD_LAUNCH_CHECK();
-  // 2. destination side: dA, alpha~, softmax backward, dt
-  s = launch_msg_x<XT>(kf_fu(F), x, F, Fu, ldx, rowptr, col, N, plan, st, stats, g, whdr, bhi,
-                       blo, slope, dp, seed, uhub, dpre, alpha_d, dt, cpart, hadot, stream);
-  if (s != GFD_OK) return s;
-  // 3. source side: dh' rows (and, fused, the grad_W' GEMM)
   const bool xvec = ldx % 4 == 0 &&
                     reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
+  const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr);
+  // 2. column maxima of |x| (k_gw's scales) and, unfused, grad_bias's column
+  // partials: on the side stream when there is one, beside step 3
+  GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
+  SideStream* side = side_stream();
+  std::unique_lock<std::mutex> side_lock;
+  hipStream_t aux = stream;
+  if (side) {
+    side_lock = std::unique_lock<std::mutex>(side->mu);
+    GFD_HIP_CHECK(hipEventRecord(side->fork, stream));
+    GFD_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
+    aux = side->s;
+  }
   {
     int64_t blocks = (N + 3) / 4;
     if (blocks > 16384) blocks = 16384;
-    GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
     const unsigned xb = unsigned(blocks < 2048 ? blocks : 2048);
     if (xvec)
-      k_xmax<XT, true><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
+      k_xmax<XT, true><<<xb, 256, 0, aux>>>(x, N, F, ldx, amax);
     else
-      k_xmax<XT, false><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
+      k_xmax<XT, false><<<xb, 256, 0, aux>>>(x, N, F, ldx, amax);
     GFD_LAUNCH_CHECK();
   }
-  const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr);
+  const bool colsum_early = grad_bias && fp.S == 0;
+  if (colsum_early) {
+    k_colsum64<<<kRedBlocks, 256, 0, aux>>>(g, N, gbp, nullptr);
+    GFD_LAUNCH_CHECK();
+  }
+  if (side) GFD_HIP_CHECK(hipEventRecord(side->join, side->s));
+  // 3. destination side: dA, alpha~, softmax backward, dt
+  s = launch_msg_x<XT>(kf_fu(F), x, F, Fu, ldx, rowptr, col, N, plan, st, stats, g, whdr, bhi,
+                       blo, slope, dp, seed, uhub, dpre, alpha_d, dt, cpart, hadot, stream);
+  if (s != GFD_OK) return s;
+  if (side) {
+    GFD_HIP_CHECK(hipStreamWaitEvent(stream, side->join, 0));
+    side_lock.unlock();
+  }
+  // 4. source side: dh' rows (and, fused, the grad_W' GEMM)
   if (fp.S > 0) {
     // source hubs first: their dh' rows, compact, at the start of the dh region
     if (shubs > 0) {
@@ -2178,10 +2275,11 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
     k_slab_bounds<<<1, 1024, 0, stream>>>(cost, fp.nt, fp.S, N, pre, bounds);
     GFD_LAUNCH_CHECK();
     const int Fu16 = (F + 15) / 16 * 16;
-    const size_t smem = size_t(flay(Fu16).bytes);
-    auto kern = xvec ? &k_src_gw<XT, true, 6> : &k_src_gw<XT, false, 6>;
+    const size_t smem = size_t(flay(Fu16, fp.NW).bytes);
+    auto kern = fp.NW == 16 ? (xvec ? &k_src_gw<XT, true, 3, 16> : &k_src_gw<XT, false, 3, 16>)
+                            : (xvec ? &k_src_gw<XT, true, 6, 8> : &k_src_gw<XT, false, 6, 8>);
     if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
-    kern<<<unsigned(16 * ((fp.S + 7) / 8)), 512, smem, stream>>>(
+    kern<<<unsigned(16 * ((fp.S + 7) / 8)), 64 * fp.NW, smem, stream>>>(
         colptr, csc_dst, csc_eid, shr, dh, alpha_d, dt, g, dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f,
         x, ldx, F, Fu16, bounds, fp.S, amax, slab);
     GFD_LAUNCH_CHECK();
@@ -2210,7 +2308,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
                                                           dh, amax, erow, 0);
       GFD_LAUNCH_CHECK();
     }
-    // 4. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
+    // 5. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
     int64_t kps = (N + gw_slabs(N) - 1) / gw_slabs(N);
     kps = (kps + kGK - 1) / kGK * kGK;
     const int64_t z = (N + kps - 1) / kps;
@@ -2231,16 +2329,12 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
     k_att_grad<<<(2 * HC + 255) / 256, 256, 0, stream>>>(W, F, gw, grad_as, grad_ad);
     GFD_LAUNCH_CHECK();
   }
-  // 5. grad_bias = sum_i g_i (the fused path's k_colsum64 already ran)
+  // 6. grad_bias = sum_i g_i (column partials: step 2 or the fused path's k_colsum64)
   if (grad_bias) {
-    if (fp.S == 0) {
-      k_colsum64<<<kRedBlocks, 256, 0, stream>>>(g, N, gbp, nullptr);
-      GFD_LAUNCH_CHECK();
-    }
     k_reduce_few<<<1, 1024, 0, stream>>>(gbp, kRedBlocks, 64, grad_bias);
     GFD_LAUNCH_CHECK();
   }
-  // 6. grad_x = dh W  (A = dh [N, 512] at row stride 528, B = W [512, F])
+  // 7. grad_x = dh W  (A = dh [N, 512] at row stride 528, B = W [512, F])
   if (grad_x && F <= 16 * kGxNT) {
     int64_t nb = ((N + 15) / 16 + 7) / 8;
     if (nb > cu_count()) nb = cu_count();

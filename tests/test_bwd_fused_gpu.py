@@ -18,9 +18,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True)
-def _fused(monkeypatch):
-    monkeypatch.setenv("GFD_BWD_FUSED", "1")  # read by libgfd on every backward call
+@pytest.fixture(autouse=True, params=["1", "2"], ids=["w8", "w16"])
+def _fused(monkeypatch, request):
+    # read by libgfd on every backward call: 1 = 8-wave blocks, 2 = 16-wave blocks
+    monkeypatch.setenv("GFD_BWD_FUSED", request.param)
 
 
 def _param_grads(x, graph_or_ei, conv, g, p=0.0, seed=0):
