@@ -31,11 +31,6 @@
 //   k_colsum64    grad_bias = column sums of g (fixed-grid partials)
 //   k_gx / k_gemm grad_x = dh W (only when requested; f16 MFMA for F <= 64)
 // Deterministic: no float atomics anywhere; every sum has a fixed order.
-#include <cstdlib>
-#include <map>
-#include <memory>
-#include <mutex>
-
 #include "gfd_check.h"
 #include "gfd_fwd.h"
 
@@ -2136,40 +2131,6 @@ gfd_status launch_msg_x(int KF, const void* x, int F, int Fu, int64_t ldx, const
 #undef GFD_MSG
 }
 
-// A non-blocking side stream per device for the passes that need neither the
-// destination pass nor the source pass (k_xmax: x only; k_colsum64: g only).
-// They fork from the caller's stream after the amax reset and join it before
-// the source pass, running beside k_bwd_msg -- whose one block per CU leaves
-// HBM bandwidth idle during its U phase.  The fork / join enqueue sequence of
-// one call holds the device's lock (it never waits on the device); under
-// stream capture the fork is captured as a cross-stream dependency.
-// GFD_BWD_SIDE=0: everything on the caller's stream (A/B).
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  std::mutex mu;
-};
-
-SideStream* side_stream() {
-  const char* e = getenv("GFD_BWD_SIDE");
-  if (e && e[0] == '0') return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  static std::mutex mu;
-  static std::map<int, std::unique_ptr<SideStream>> per_dev;
-  std::lock_guard<std::mutex> g(mu);
-  std::unique_ptr<SideStream>& p = per_dev[dev];
-  if (!p) {
-    std::unique_ptr<SideStream> n(new SideStream);
-    if (hipStreamCreateWithFlags(&n->s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&n->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&n->join, hipEventDisableTiming) != hipSuccess)
-      return nullptr;
-    p = std::move(n);
-  }
-  return p.get();
-}
-
 template <typename XT>
 gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
                     const int32_t* col, const gfd_plan* plan, const int32_t* colptr,
@@ -2209,46 +2170,25 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   const int64_t nfr = int64_t(H) * 2 * NT * 64;
   k_bwd_wpack<<<unsigned((nfr + 255) / 256), 256, 0, stream>>>(W, F, NT, whdr, bhi, blo);
   GFD_LAUNCH_CHECK();
-  const bool xvec = ldx % 4 == 0 &&
-                    reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
-  const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr);
-  // 2. column maxima of |x| (k_gw's scales) and, unfused, grad_bias's column
-  // partials: on the side stream when there is one, beside step 3
-  GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
-  SideStream* side = side_stream();
-  std::unique_lock<std::mutex> side_lock;
-  hipStream_t aux = stream;
-  if (side) {
-    side_lock = std::unique_lock<std::mutex>(side->mu);
-    GFD_HIP_CHECK(hipEventRecord(side->fork, stream));
-    GFD_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
-    aux = side->s;
-  }
-  {
-    int64_t blocks = (N + 3) / 4;
-    if (blocks > 16384) blocks = 16384;
-    const unsigned xb = unsigned(blocks < 2048 ? blocks : 2048);
-    if (xvec)
-      k_xmax<XT, true><<<xb, 256, 0, aux>>>(x, N, F, ldx, amax);
-    else
-      k_xmax<XT, false><<<xb, 256, 0, aux>>>(x, N, F, ldx, amax);
-    GFD_LAUNCH_CHECK();
-  }
-  const bool colsum_early = grad_bias && fp.S == 0;
-  if (colsum_early) {
-    k_colsum64<<<kRedBlocks, 256, 0, aux>>>(g, N, gbp, nullptr);
-    GFD_LAUNCH_CHECK();
-  }
-  if (side) GFD_HIP_CHECK(hipEventRecord(side->join, side->s));
-  // 3. destination side: dA, alpha~, softmax backward, dt
+  // 2. destination side: dA, alpha~, softmax backward, dt
   s = launch_msg_x<XT>(kf_fu(F), x, F, Fu, ldx, rowptr, col, N, plan, st, stats, g, whdr, bhi,
                        blo, slope, dp, seed, uhub, dpre, alpha_d, dt, cpart, hadot, stream);
   if (s != GFD_OK) return s;
-  if (side) {
-    GFD_HIP_CHECK(hipStreamWaitEvent(stream, side->join, 0));
-    side_lock.unlock();
+  // 3. source side: dh' rows (and, fused, the grad_W' GEMM)
+  const bool xvec = ldx % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
+  {
+    int64_t blocks = (N + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
+    GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
+    const unsigned xb = unsigned(blocks < 2048 ? blocks : 2048);
+    if (xvec)
+      k_xmax<XT, true><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
+    else
+      k_xmax<XT, false><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
+    GFD_LAUNCH_CHECK();
   }
-  // 4. source side: dh' rows (and, fused, the grad_W' GEMM)
+  const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr);
   if (fp.S > 0) {
     // source hubs first: their dh' rows, compact, at the start of the dh region
     if (shubs > 0) {
@@ -2308,7 +2248,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
                                                           dh, amax, erow, 0);
       GFD_LAUNCH_CHECK();
     }
-    // 5. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
+    // 4. grad_W' = dh'^T x  (rows 0..511 grad_W, 512.. S, 520.. T)
     int64_t kps = (N + gw_slabs(N) - 1) / gw_slabs(N);
     kps = (kps + kGK - 1) / kGK * kGK;
     const int64_t z = (N + kps - 1) / kps;
@@ -2329,12 +2269,16 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
     k_att_grad<<<(2 * HC + 255) / 256, 256, 0, stream>>>(W, F, gw, grad_as, grad_ad);
     GFD_LAUNCH_CHECK();
   }
-  // 6. grad_bias = sum_i g_i (column partials: step 2 or the fused path's k_colsum64)
+  // 5. grad_bias = sum_i g_i (the fused path's k_colsum64 already ran)
   if (grad_bias) {
+    if (fp.S == 0) {
+      k_colsum64<<<kRedBlocks, 256, 0, stream>>>(g, N, gbp, nullptr);
+      GFD_LAUNCH_CHECK();
+    }
     k_reduce_few<<<1, 1024, 0, stream>>>(gbp, kRedBlocks, 64, grad_bias);
     GFD_LAUNCH_CHECK();
   }
-  // 7. grad_x = dh W  (A = dh [N, 512] at row stride 528, B = W [512, F])
+  // 6. grad_x = dh W  (A = dh [N, 512] at row stride 528, B = W [512, F])
   if (grad_x && F <= 16 * kGxNT) {
     int64_t nb = ((N + 15) / 16 + 7) / 8;
     if (nb > cu_count()) nb = cu_count();
