@@ -21,7 +21,20 @@ __global__ void __launch_bounds__(1024) k_wmax(const float* __restrict__ W, int 
   const int t = threadIdx.x;
   const int n = H * C * F;
   float m0 = 0.f, m1 = 0.f;
-  for (int i = t; i < n; i += 1024) m0 = fmaxf(m0, fabsf(W[i]));
+  // (latency-bound on one block: 16-B loads, eight in flight per thread)
+  if (reinterpret_cast<uintptr_t>(W) % 16 == 0) {
+    const f32x4* W4 = reinterpret_cast<const f32x4*>(W);
+    const int n4 = n / 4;  // n = 512 F: a multiple of 4
+#pragma unroll 8
+    for (int i = t; i < n4; i += 1024) {
+      const f32x4 v = W4[i];
+      m0 = fmaxf(m0, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+#pragma unroll 8
+    for (int i = t; i < n; i += 1024) m0 = fmaxf(m0, fabsf(W[i]));
+  }
+#pragma unroll 2
   for (int i = t; i < C * F; i += 1024) {  // Wbar[c][f] = mean_h W[h C + c][f]
     float s = 0.f;
 #pragma unroll
