@@ -99,31 +99,12 @@ __global__ void __launch_bounds__(256) k_hub_fin(const float* __restrict__ part,
 #pragma unroll
   for (int q = 1; q < H; ++q)
     if (hh == q) { Mh = M[q]; Sh = S[q]; }
-  // the hub's chunks in rounds of 16 (their loads issued together; a large
-  // hub's ~700 chunk partials are otherwise one long chain of dependent
-  // round trips -- the stage's critical path on a shard), four accumulators
-  // in a fixed order
-  f32x4 acc4[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int c = c0;
-  for (; c + 16 <= c1; c += 16) {
-    f32x4 v[16];
-    float e[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const float* pr = part + int64_t(c + u) * stride;
-      v[u] = reinterpret_cast<const f32x4*>(pr + 16)[k4];
-      e[u] = pr[hh];
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) acc4[u & 3] += v[u] * __expf(e[u] - Mh);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int c = c0; c < c1; ++c) {
+    const float* pr = part + c * stride;
+    acc += reinterpret_cast<const f32x4*>(pr + 16)[k4] * __expf(pr[hh] - Mh);
   }
-  for (; c < c1; ++c) {
-    const float* pr = part + int64_t(c) * stride;
-    acc4[0] += reinterpret_cast<const f32x4*>(pr + 16)[k4] * __expf(pr[hh] - Mh);
-  }
-  const f32x4 acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
   reinterpret_cast<f32x4*>(zhub + hb * KP)[k4] = acc * (1.0f / (Sh + kSoftmaxEps));
 }
 
