@@ -340,7 +340,14 @@ k_logits_lone(
             for (int i = 0; i < 4; ++i) dst[i] = v[i];
           }
         };
+#ifdef GFD_AB_LOGITS_S64  // ablation only (wrong results: the 8 floats before s overwritten): 64-B s blocks
+        if (qd < 2) {
+          put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd - 8);
+          put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd);
+        }
+#else
         if (qd < 2) put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd);
+#endif
         else put(tl + uint64_t(uint32_t(orow)) * uint32_t(ldt) + 4 * (qd - 2));
       }
     }
