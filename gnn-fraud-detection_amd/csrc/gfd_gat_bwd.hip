@@ -726,13 +726,15 @@ __global__ void __launch_bounds__(256) k_bwd_src(
   amax_commit(cm, ct, amax);
 }
 
-// Per-column maxima of |x| (amax[kDH + f]): one wave per row in a grid-stride
+// Per-column maxima of |x| (amax[off + f]; off = kDH in the workspace record,
+// 0 for gfd_x_colmax): one wave per row in a grid-stride
 // loop, lane = 4-column chunk (16-B fp32 / 8-B bf16 loads when rows allow
 // them, VEC; else one column per lane and q), four rows' loads in flight;
 // block maxima in LDS, then one conditional atomic per column.
 template <typename XT, bool VEC>
 __global__ void __launch_bounds__(256) k_xmax(const typename XT::T* __restrict__ x, int64_t N,
-                                              int F, int64_t ldx, uint32_t* __restrict__ amax) {
+                                              int F, int64_t ldx, uint32_t* __restrict__ amax,
+                                              int off) {
   __shared__ float red[4][kXCols];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nw = int64_t(gridDim.x) * 4;
@@ -768,7 +770,7 @@ __global__ void __launch_bounds__(256) k_xmax(const typename XT::T* __restrict__
   for (int q = 0; q < 4; ++q) red[w][col(q)] = xm[q];  // col(q) < 256 = kXCols
   __syncthreads();
   for (int f = threadIdx.x; f < F; f += blockDim.x)
-    amax_put(amax, kDH + f, fmaxf(fmaxf(red[0][f], red[1][f]), fmaxf(red[2][f], red[3][f])));
+    amax_put(amax, off + f, fmaxf(fmaxf(red[0][f], red[1][f]), fmaxf(red[2][f], red[3][f])));
 }
 
 // source hub chunks {hub, p0, p1, src}: partial y (512) | ds (8) per chunk
@@ -2132,13 +2134,27 @@ gfd_status launch_msg_x(int KF, const void* x, int F, int Fu, int64_t ldx, const
 }
 
 template <typename XT>
+gfd_status launch_xmax(const typename XT::T* x, int64_t N, int F, int64_t ldx, bool xvec,
+                       uint32_t* amax, int off, hipStream_t stream) {
+  int64_t blocks = (N + 3) / 4;
+  if (blocks > 16384) blocks = 16384;
+  const unsigned xb = unsigned(blocks < 2048 ? blocks : 2048);
+  if (xvec)
+    k_xmax<XT, true><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax, off);
+  else
+    k_xmax<XT, false><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax, off);
+  GFD_LAUNCH_CHECK();
+  return GFD_OK;
+}
+
+template <typename XT>
 gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, const int32_t* rowptr,
                     const int32_t* col, const gfd_plan* plan, const int32_t* colptr,
                     const int32_t* csc_dst, const int32_t* csc_eid, const gfd_plan* src_plan,
                     int64_t M, const float* W, const float* att_src, const float* att_dst,
                     float slope, float dp, uint64_t seed, const float* st, const float* stats,
                     const float* g, float* grad_x, float* grad_W, float* grad_as, float* grad_ad,
-                    float* grad_bias, void* ws, hipStream_t stream) {
+                    float* grad_bias, const uint32_t* xcm, void* ws, hipStream_t stream) {
   const int64_t hubs = plan ? plan->num_hubs : 0, chunks = plan ? plan->num_chunks : 0;
   const int64_t shubs = src_plan ? src_plan->num_hubs : 0;
   const int64_t schunks = src_plan ? src_plan->num_chunks : 0;
@@ -2177,16 +2193,13 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
   // 3. source side: dh' rows (and, fused, the grad_W' GEMM)
   const bool xvec = ldx % 4 == 0 &&
                     reinterpret_cast<uintptr_t>(x) % (4 * sizeof(typename XT::T)) == 0;
-  {
-    int64_t blocks = (N + 3) / 4;
-    if (blocks > 16384) blocks = 16384;
-    GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
-    const unsigned xb = unsigned(blocks < 2048 ? blocks : 2048);
-    if (xvec)
-      k_xmax<XT, true><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
-    else
-      k_xmax<XT, false><<<xb, 256, 0, stream>>>(x, N, F, ldx, amax);
-    GFD_LAUNCH_CHECK();
+  GFD_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(uint32_t) * kAmaxCols, stream));
+  if (xcm) {  // the caller's maxima of this x (gfd_x_colmax, e.g. once per x version)
+    GFD_HIP_CHECK(hipMemcpyAsync(amax + kDH, xcm, sizeof(uint32_t) * F, hipMemcpyDeviceToDevice,
+                                 stream));
+  } else {
+    const gfd_status xs = launch_xmax<XT>(x, N, F, ldx, xvec, amax, kDH, stream);
+    if (xs != GFD_OK) return xs;
   }
   const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr);
   if (fp.S > 0) {
@@ -2304,14 +2317,15 @@ size_t gfd_gat_bwd_workspace_size(int64_t N, int64_t M, int F, int heads, int ch
   return s.off;
 }
 
-gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
+gfd_status gfd_gat_bwd_ex(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
                        const int32_t* rowptr, const int32_t* col, const gfd_plan* plan,
                        const int32_t* colptr, const int32_t* csc_dst, const int32_t* csc_eid,
                        const gfd_plan* src_plan, int64_t M, const float* W, const float* att_src,
                        const float* att_dst, int heads, int channels, float slope, float dp,
                        uint64_t seed, const float* st, const float* stats, const float* g,
                        float* grad_x, float* grad_W, float* grad_as, float* grad_ad,
-                       float* grad_bias, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+                          float* grad_bias, const uint32_t* x_colmax, void* ws, size_t ws_bytes,
+                          gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (heads != H || channels != C || F < 1 || F > 256) return GFD_ERR_UNSUPPORTED;
   if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
@@ -2342,10 +2356,44 @@ gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ld
   if (x_dtype == GFD_DTYPE_BF16)
     return bwd_impl<XBF16>(static_cast<const uint16_t*>(xv), N, F, ldx, rowptr, col, plan, colptr,
                     csc_dst, csc_eid, src_plan, M, W, att_src, att_dst, slope, dp, seed, st, stats,
-                    g, grad_x, grad_W, grad_as, grad_ad, grad_bias, ws, stream);
+                    g, grad_x, grad_W, grad_as, grad_ad, grad_bias, x_colmax, ws, stream);
   return bwd_impl<XF32>(static_cast<const float*>(xv), N, F, ldx, rowptr, col, plan, colptr, csc_dst,
                   csc_eid, src_plan, M, W, att_src, att_dst, slope, dp, seed, st, stats, g, grad_x,
-                  grad_W, grad_as, grad_ad, grad_bias, ws, stream);
+                  grad_W, grad_as, grad_ad, grad_bias, x_colmax, ws, stream);
+}
+
+
+gfd_status gfd_gat_bwd(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
+                       const int32_t* rowptr, const int32_t* col, const gfd_plan* plan,
+                       const int32_t* colptr, const int32_t* csc_dst, const int32_t* csc_eid,
+                       const gfd_plan* src_plan, int64_t M, const float* W, const float* att_src,
+                       const float* att_dst, int heads, int channels, float slope, float dp,
+                       uint64_t seed, const float* st, const float* stats, const float* g,
+                       float* grad_x, float* grad_W, float* grad_as, float* grad_ad,
+                       float* grad_bias, void* ws, size_t ws_bytes, gfd_stream_t stream) {
+  return gfd_gat_bwd_ex(xv, x_dtype, N, F, ldx, rowptr, col, plan, colptr, csc_dst, csc_eid,
+                        src_plan, M, W, att_src, att_dst, heads, channels, slope, dp, seed, st,
+                        stats, g, grad_x, grad_W, grad_as, grad_ad, grad_bias, nullptr, ws,
+                        ws_bytes, stream);
+}
+
+gfd_status gfd_x_colmax(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
+                        uint32_t* colmax, gfd_stream_t stream_) {
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (F < 1 || F > 256) return GFD_ERR_UNSUPPORTED;
+  if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
+  if (N <= 0 || !xv || !colmax || ldx < F) return GFD_ERR_ARGUMENT;
+  if (N > 0x7fffffff || ldx * (x_dtype == GFD_DTYPE_BF16 ? 2 : 4) > 0xffffffffLL)
+    return GFD_ERR_UNSUPPORTED;
+  GFD_HIP_CHECK(hipMemsetAsync(colmax, 0, sizeof(uint32_t) * F, stream));
+  if (x_dtype == GFD_DTYPE_BF16) {
+    const uint16_t* x = static_cast<const uint16_t*>(xv);
+    const bool vec = ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 8 == 0;
+    return launch_xmax<XBF16>(x, N, F, ldx, vec, colmax, 0, stream);
+  }
+  const float* x = static_cast<const float*>(xv);
+  const bool vec = ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
+  return launch_xmax<XF32>(x, N, F, ldx, vec, colmax, 0, stream);
 }
 
 }  // extern "C"

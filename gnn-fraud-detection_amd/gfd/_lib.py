@@ -126,6 +126,10 @@ SIGNATURES = {
     "gfd_gat_bwd": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, PLAN, P, P, P, PLAN, c_i64,
                             P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P, P, P, P, P,
                             P, P, c_sz, P]),
+    "gfd_gat_bwd_ex": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, PLAN, P, P, P, PLAN,
+                               c_i64, P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P,
+                               P, P, P, P, P, P, P, c_sz, P]),
+    "gfd_x_colmax": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P]),
 }
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "edge index out of range", 3: "workspace too small",

@@ -15,6 +15,8 @@ Forward and backward both run in libgfd.so (``gfd_gat_fwd`` /
 from __future__ import annotations
 
 import math
+import weakref
+from collections import OrderedDict
 from typing import Optional
 
 import torch
@@ -104,17 +106,44 @@ class GATConvFunction(torch.autograd.Function):
         plan, splan = graph.plan(), csc.plan
         ws = _ws(lib.gfd_gat_bwd_workspace_size(N, graph.num_messages, F, H, C, plan.num_hubs,
                                                 plan.num_chunks, splan.num_chunks), dev)
-        _lib.call("gfd_gat_bwd", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+        cm = x_colmax(x)
+        _lib.call("gfd_gat_bwd_ex", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
                   graph.rowptr.data_ptr(), graph.col.data_ptr(), plan.cstruct(),
                   csc.colptr.data_ptr(), csc.dst.data_ptr(), csc.eid.data_ptr(), splan.cstruct(),
                   graph.num_messages, weight.data_ptr(), att_src.data_ptr(),
                   att_dst.data_ptr(), H, C, slope, dp, seed & (2 ** 64 - 1), st.data_ptr(),
                   stats.data_ptr(), g.data_ptr(), _lib.ptr(gx), gw.data_ptr(), gas.data_ptr(),
-                  gad.data_ptr(), _lib.ptr(gb), ws.data_ptr(), ws.numel(),
+                  gad.data_ptr(), _lib.ptr(gb), cm.data_ptr(), ws.data_ptr(), ws.numel(),
                   _lib.stream_handle(dev))
         if gx is not None and x.dtype != torch.float32:
             gx = gx.to(x.dtype)
         return gx, gw, gas, gad, gb, None, None, None, None, None
+
+
+# Per-column maxima of |x| -- the scales of the backward's grad_W GEMM -- kept
+# per version of the x tensor: the first layer's input is the same features
+# tensor every training step (train.py:115-143), so gfd_x_colmax runs once for
+# it.  Keyed on the tensor object (a weak reference: a new tensor at a recycled
+# address is a different object) and its version counter (in-place updates).
+_COLMAX: "OrderedDict[int, tuple]" = OrderedDict()
+_COLMAX_ENTRIES = 8
+
+
+def x_colmax(x: torch.Tensor) -> torch.Tensor:
+    """uint32 [F] max |x[:, f]| as float bits (gfd_x_colmax), cached per x version."""
+    ent = _COLMAX.get(id(x))
+    if ent is not None:
+        ref, ver, ptr, cm = ent
+        if ref() is x and ver == x._version and ptr == x.data_ptr():
+            _COLMAX.move_to_end(id(x))
+            return cm
+    cm = torch.empty(x.size(1), dtype=torch.int32, device=x.device)
+    _lib.call("gfd_x_colmax", x.data_ptr(), _lib.x_dtype_code(x), x.size(0), x.size(1),
+              x.stride(0), cm.data_ptr(), _lib.stream_handle(x.device))
+    _COLMAX[id(x)] = (weakref.ref(x), x._version, x.data_ptr(), cm)
+    while len(_COLMAX) > _COLMAX_ENTRIES:
+        _COLMAX.popitem(last=False)
+    return cm
 
 
 def gat_conv(x: torch.Tensor, edge_index_or_graph, weight: torch.Tensor, att_src: torch.Tensor,

@@ -478,6 +478,29 @@ gfd_status gfd_gat_bwd(const void* x, int x_dtype, int64_t num_nodes, int in_fea
                        float* grad_att_src, float* grad_att_dst, float* grad_bias, void* ws,
                        size_t ws_bytes, gfd_stream_t stream);
 
+/* gfd_gat_bwd with the per-column maxima of |x| supplied (ABI 6): x_colmax
+ * (nullable = computed inside, as gfd_gat_bwd does) is uint32 [in_features]
+ * holding max_n |x[n][f]| as float bits, from gfd_x_colmax over the same x.
+ * The grad_W GEMM scales each x column by a power of two from it.  A layer
+ * input that stays the same across training steps (the first layer's
+ * features, train.py:115-143) needs it once per version of x. */
+gfd_status gfd_gat_bwd_ex(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                          int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                          const gfd_plan* plan, const int32_t* colptr, const int32_t* csc_dst,
+                          const int32_t* csc_eid, const gfd_plan* src_plan,
+                          int64_t num_messages, const float* weight, const float* att_src,
+                          const float* att_dst, int heads, int channels, float negative_slope,
+                          float dropout_p, uint64_t dropout_seed, const float* st,
+                          const float* stats, const float* grad_out, float* grad_x,
+                          float* grad_weight, float* grad_att_src, float* grad_att_dst,
+                          float* grad_bias, const uint32_t* x_colmax, void* ws, size_t ws_bytes,
+                          gfd_stream_t stream);
+
+/* Per-column maxima of |x| over rows [0, num_nodes) as float bits into
+ * colmax (uint32 [in_features], in_features <= 256), for gfd_gat_bwd_ex. */
+gfd_status gfd_x_colmax(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                        int64_t x_stride, uint32_t* colmax, gfd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Training-mode layer body (gat.py:82-91, tgn.py:96-105):
  *   out = residual + dropout(relu(BatchNorm1d_train(y)))
