@@ -48,6 +48,13 @@ constexpr int kRedBlocks = 1024;   // fixed grid of the column-sum partial kerne
 // Per-message record (64 B, edge order): alpha~ [8] | dpre [8] -- the source
 // side reads both halves of one line per message, not two lines
 constexpr int kRec = 16;
+// k_bwd_msg, GFD_BWD_WPRE=1: a head group's W fragments loaded together, ahead
+// of its MFMAs (group 0's behind the G rows, group 1's across group 0's LDS
+// round trip) -- measured 1.0-1.4 ms SLOWER than loading them per piece
+// (profiles/r5i_bwd_fused_w16_and_side_stream.txt), so off
+#ifndef GFD_BWD_WPRE
+#define GFD_BWD_WPRE 0
+#endif
 
 __device__ __forceinline__ float ldx1(const float* p) { return *p; }
 __device__ __forceinline__ float ldx1(const uint16_t* p) { return __uint_as_float(uint32_t(*p) << 16); }
@@ -409,11 +416,35 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
     }
     return;
   }
+  // head group 0's W fragments in flight while the G tile is prepared; group
+  // 1's are issued behind group 0's MFMAs (two L2 round trips per block
+  // instead of one per piece and head group).  KF = 4 (F > 192): per piece
+  // (the prefetched set would spill)
+  constexpr bool kWPre = GFD_BWD_WPRE && KF <= 3;
+  uint4 wh[PM][2], wl[PM][2];
+  auto load_w = [&](int hg) {  // branch-free: a piece past the last loads piece 0's fragments
+#pragma unroll
+    for (int pi = 0; pi < PM; ++pi) {
+      const int pc = w + kUW * pi < 4 * NT ? pi : 0;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) wfrag(hg, pc, s, wh[pi][s], wl[pi][s]);
+    }
+  };
+  // the G rows first: vector-memory counters retire in order, so loads issued
+  // ahead of them would be waited for too
+  float gvr[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)  // branch-free (an empty slot reads row 0; dropped below)
+    gvr[d] = g[int64_t(dsc[d].x >= 0 ? dsc[d].x : 0) * C + lane];
+  if constexpr (kWPre) {
+    __builtin_amdgcn_sched_barrier(0);  // keep the G loads first
+    load_w(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
     // G row: power-of-two scaled, fp16 hi / lo'
-    const int i = dsc[d].x;
-    const float gv = i >= 0 ? g[int64_t(i) * C + lane] : 0.f;
+    const float gv = dsc[d].x >= 0 ? gvr[d] : 0.f;
     const int er = scale_exp(max_wave(fabsf(gv)));
     const float t = gv * ldexpf(1.0f, er);
     const _Float16 th = (_Float16)t;
@@ -447,7 +478,12 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         uint4 bh, bl;
-        wfrag(hg, pi, s, bh, bl);
+        if constexpr (kWPre) {
+          bh = wh[pi][s];
+          bl = wl[pi][s];
+        } else {
+          wfrag(hg, pi, s, bh, bl);
+        }
 #pragma unroll
         for (int rg = 0; rg < 2; ++rg) {
           const int ao = (16 * rg + (lane & 15)) * kGS + 32 * s + 8 * (lane >> 4);
@@ -464,6 +500,7 @@ __global__ void __launch_bounds__(kUW * 64) k_bwd_msg(
         }
       }
     }
+    if (kWPre && hg == 0) load_w(1);  // in flight across the U tile's LDS round trip
     __syncthreads();
 #pragma unroll
     for (int d = 0; d < 2; ++d)
