@@ -253,19 +253,22 @@ gfd_status gfd_gat_aggregate(const void* x, int x_dtype, int64_t N, int F, int64
                               stages, out, stats, ws, ws_bytes, stream_);
 }
 
-gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+// gfd_gat_fwd_ep with the packed weights either built here (packed_in NULL:
+// weight / att_* packed into the workspace) or supplied (gfd_gat_fwd_ep_packed)
+static gfd_status fwd_ep_impl(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
                           const int32_t* rowptr, const int32_t* col, const float* weight,
                           const float* att_src, const float* att_dst, const float* bias,
                           int heads, int channels, float slope, float dp, uint64_t seed,
                           const gfd_plan* plan, const gfd_epilogue* ep, float* out, float* st,
-                          float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+                          float* stats, void* ws, size_t ws_bytes, const void* packed_in,
+                          gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (!check_hc(heads, channels, F)) return GFD_ERR_UNSUPPORTED;
   const gfd_plan p = plan_or_empty(plan);
   if (!out && ep && ep->head_out) out = ep->head_out;  // rows not written: the head replaces them
   gfd_status s = check_agg_args(x, x_dtype, N, F, ldx, rowptr, col, N, 0, dp, p, out);
   if (s != GFD_OK) return s;
-  if (!weight || !att_src || !att_dst) return GFD_ERR_ARGUMENT;
+  if (!packed_in && (!weight || !att_src || !att_dst)) return GFD_ERR_ARGUMENT;
   Epi e{nullptr, 0, nullptr, 0};
   if (ep) {  // inference epilogue: no training statistics, no dropout
     if (!ep->scale_shift || stats || dp > 0.f) return GFD_ERR_ARGUMENT;
@@ -283,7 +286,8 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
   AggArgs a{x, x_dtype, F, ldx, N, rowptr, col, N, 0, st, 16, st ? st + H : nullptr, 16, nullptr,
             bias, slope, dp, seed, p, GFD_STAGE_ALL, out, stats, nullptr, nullptr, nullptr, e};
   hub_ws_layout(&c, p.num_hubs, p.num_chunks, L, &a.part, &a.zhub);
-  void* packed = c.take<char>(L.bytes);
+  void* packed_ws = c.take<char>(L.bytes);
+  const void* packed = packed_in ? packed_in : packed_ws;
   float* st_ws = c.take<float>(size_t(N) * 16);
   float* xmax = c.take<float>(1);
   if (!c.ok) return GFD_ERR_WORKSPACE;
@@ -294,8 +298,10 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
   a.xmax = xmax;
   s = check_graph(rowptr, col, N, N, plan, nullptr, nullptr, nullptr, 0, stream);
   if (s != GFD_OK) return s;
-  s = gfd_gat_pack_weights(weight, att_src, att_dst, F, heads, channels, packed, stream_);
-  if (s != GFD_OK) return s;
+  if (!packed_in) {
+    s = gfd_gat_pack_weights(weight, att_src, att_dst, F, heads, channels, packed_ws, stream_);
+    if (s != GFD_OK) return s;
+  }
   if (hipMemsetAsync(xmax, 0, sizeof(float), stream) != hipSuccess) return GFD_ERR_HIP;
   if (lone_fusable(a, L)) {
     // the lone destinations' outputs come out of the logits pass; the tile
@@ -309,6 +315,29 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t 
     if (s != GFD_OK) return s;
   }
   return aggregate_impl(a, stream);
+}
+
+gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+                          const int32_t* rowptr, const int32_t* col, const float* weight,
+                          const float* att_src, const float* att_dst, const float* bias,
+                          int heads, int channels, float slope, float dp, uint64_t seed,
+                          const gfd_plan* plan, const gfd_epilogue* ep, float* out, float* st,
+                          float* stats, void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+  return fwd_ep_impl(x, x_dtype, N, F, ldx, rowptr, col, weight, att_src, att_dst, bias, heads,
+                     channels, slope, dp, seed, plan, ep, out, st, stats, ws, ws_bytes, nullptr,
+                     stream_);
+}
+
+gfd_status gfd_gat_fwd_ep_packed(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,
+                                 const int32_t* rowptr, const int32_t* col, const void* packed,
+                                 const float* bias, int heads, int channels, float slope,
+                                 float dp, uint64_t seed, const gfd_plan* plan,
+                                 const gfd_epilogue* ep, float* out, float* st, float* stats,
+                                 void* ws, size_t ws_bytes, gfd_stream_t stream_) {
+  if (!packed) return GFD_ERR_ARGUMENT;
+  return fwd_ep_impl(x, x_dtype, N, F, ldx, rowptr, col, nullptr, nullptr, nullptr, bias, heads,
+                     channels, slope, dp, seed, plan, ep, out, st, stats, ws, ws_bytes, packed,
+                     stream_);
 }
 
 gfd_status gfd_gat_fwd(const void* x, int x_dtype, int64_t N, int F, int64_t ldx,

@@ -109,6 +109,9 @@ SIGNATURES = {
     "gfd_gat_fwd_ep": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, P, P, ct.c_int,
                                ct.c_int, c_f32, c_f32, c_u64, PLAN, ct.POINTER(GfdEpilogue), P, P,
                                P, P, c_sz, P]),
+    "gfd_gat_fwd_ep_packed": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, P, P, ct.c_int,
+                                      ct.c_int, c_f32, c_f32, c_u64, PLAN,
+                                      ct.POINTER(GfdEpilogue), P, P, P, P, c_sz, P]),
     "gfd_gru_head": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, P, ct.c_int, P,
                              P, P]),
     "gfd_gru_head_bwd": (c_i32, [P, c_i64, ct.c_int, c_i64, P, P, P, P, P, c_i64, P, ct.c_int, P,

@@ -64,6 +64,63 @@ def head_foldable(head, width: int, conv=None) -> bool:
             (head.bias is None or head.bias.dtype == torch.float32))
 
 
+def eval_weights(conv, bn, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(packed weights, BatchNorm scale | shift) of an inference layer, rebuilt
+    only when a tensor they derive from changed: the cache on ``conv`` holds
+    each source tensor and its version counter, so a replaced parameter (a new
+    object) or an in-place update (optimizer step, load_state_dict) rebuilds
+    it, while evaluation over many batches (evaluate.py:73-98) packs once."""
+    srcs = [conv.lin_src.weight, conv.att_src, conv.att_dst]
+    if bn is not None:
+        srcs += [bn.running_mean, bn.running_var]
+        if bn.affine:
+            srcs += [bn.weight, bn.bias]
+    key = [(t, t._version) for t in srcs] + [bn.eps if bn is not None else None, bn]
+    c = conv.__dict__.get("_gfd_eval")
+    if c is not None and len(c[0]) == len(key) and all(
+            (a[0] is b[0] and a[1] == b[1]) if isinstance(a, tuple) else a is b or a == b
+            for a, b in zip(c[0], key)):
+        return c[1], c[2]
+    W = conv.lin_src.weight.detach().contiguous()
+    F = W.size(1)
+    lib = _lib.load()
+    packed = torch.empty(lib.gfd_gat_packed_size(F, H, C), dtype=torch.uint8, device=device)
+    _lib.call("gfd_gat_pack_weights", W.data_ptr(),
+              conv.att_src.detach().reshape(-1).contiguous().data_ptr(),
+              conv.att_dst.detach().reshape(-1).contiguous().data_ptr(), F, H, C,
+              packed.data_ptr(), _lib.stream_handle(device))
+    ab = bn_affine(bn, device)
+    conv.__dict__["_gfd_eval"] = (key, packed, ab)
+    return packed, ab
+
+
+def eval_conv(conv, x: torch.Tensor, edge_index) -> torch.Tensor:
+    """``conv(x, edge_index)`` in inference (no autograd, no dropout) with the
+    layer's packed weights from ``eval_weights``: the drop-in module's
+    ``torch.no_grad()`` forward (gat.py:80 under evaluate.py:73-98)."""
+    from .nn import _check_tensor
+    dev = x.device
+    _check_tensor("x", x, dev, (torch.float32, torch.bfloat16))
+    graph = edge_index if isinstance(edge_index, CSRGraph) else get_graph(edge_index, x.size(0))
+    if graph.num_nodes != x.size(0):
+        raise ValueError(f"graph has {graph.num_nodes} nodes but x has {x.size(0)} rows")
+    x = _rows(x)
+    N, F = x.shape
+    if F != conv.lin_src.weight.size(1):
+        raise ValueError(f"x has {F} features, the layer expects {conv.lin_src.weight.size(1)}")
+    packed, _ = eval_weights(conv, None, dev)
+    bias = conv.bias.detach() if conv.bias is not None else None
+    plan = graph.plan()
+    lib = _lib.load()
+    out = torch.empty((N, C), dtype=torch.float32, device=dev)
+    ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, plan.num_hubs, plan.num_chunks), dev)
+    _lib.call("gfd_gat_fwd_ep_packed", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+              graph.rowptr.data_ptr(), graph.col.data_ptr(), packed.data_ptr(), _lib.ptr(bias),
+              H, C, float(conv.negative_slope), 0.0, 0, plan.cstruct(), None, out.data_ptr(),
+              None, None, ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+    return out
+
+
 def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
               residual: bool = False, head=None) -> torch.Tensor:
     """One eval-mode layer body: residual(h) + relu(bn(conv(h, edge_index))).
@@ -76,11 +133,8 @@ def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
     graph = edge_index if isinstance(edge_index, CSRGraph) else get_graph(edge_index, h.size(0))
     x = _rows(h)
     N, F = x.shape
-    W = conv.lin_src.weight.detach().contiguous()
-    a_s = conv.att_src.detach().reshape(-1).contiguous()
-    a_d = conv.att_dst.detach().reshape(-1).contiguous()
     bias = conv.bias.detach() if conv.bias is not None else None
-    ab = bn_affine(bn, dev)
+    packed, ab = eval_weights(conv, bn, dev)
     res = None
     if residual:
         if F != C:
@@ -102,11 +156,10 @@ def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
     lib = _lib.load()
     out = torch.empty((N, C), dtype=torch.float32, device=dev) if hout is None else None
     ws = _ws(lib.gfd_gat_fwd_workspace_size(N, N, F, H, C, plan.num_hubs, plan.num_chunks), dev)
-    _lib.call("gfd_gat_fwd_ep", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
-              graph.rowptr.data_ptr(), graph.col.data_ptr(), W.data_ptr(), a_s.data_ptr(),
-              a_d.data_ptr(), _lib.ptr(bias), H, C, float(conv.negative_slope), 0.0, 0,
-              plan.cstruct(), _lib.ct.byref(ep), _lib.ptr(out), None, None, ws.data_ptr(),
-              ws.numel(), _lib.stream_handle(dev))
+    _lib.call("gfd_gat_fwd_ep_packed", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+              graph.rowptr.data_ptr(), graph.col.data_ptr(), packed.data_ptr(), _lib.ptr(bias),
+              H, C, float(conv.negative_slope), 0.0, 0, plan.cstruct(), _lib.ct.byref(ep),
+              _lib.ptr(out), None, None, ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
     return out if hout is None else hout
 
 

@@ -209,6 +209,11 @@ class GATConv(nn.Module):
     def forward(self, x: torch.Tensor, edge_index, size=None, return_attention_weights=None):
         if return_attention_weights:
             raise NotImplementedError("gfd GATConv: return_attention_weights is not supported")
+        if not torch.is_grad_enabled() and not (self.training and self.dropout > 0) and x.is_cuda:
+            # inference: the packed weights are cached while the parameters do
+            # not change (gfd.fused.eval_weights)
+            from .fused import eval_conv
+            return eval_conv(self, x, edge_index)
         return gat_conv(x, edge_index, self.lin_src.weight, self.att_src, self.att_dst, self.bias,
                         self.negative_slope, self.dropout, self.training)
 

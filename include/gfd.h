@@ -364,6 +364,18 @@ gfd_status gfd_gat_fwd_ep(const void* x, int x_dtype, int64_t num_nodes, int in_
                           const gfd_epilogue* ep, float* out, float* st, float* stats, void* ws,
                           size_t ws_bytes, gfd_stream_t stream);
 
+/* gfd_gat_fwd_ep with the weights already packed (gfd_gat_pack_weights; ABI
+ * 6): an inference caller packs a layer's weights once and reuses them while
+ * they do not change (evaluate.py:73-98 runs the same trained layers on every
+ * batch), instead of the seven small pack launches per call. */
+gfd_status gfd_gat_fwd_ep_packed(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                                 int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                                 const void* packed, const float* bias, int heads, int channels,
+                                 float negative_slope, float dropout_p, uint64_t dropout_seed,
+                                 const gfd_plan* plan, const gfd_epilogue* ep, float* out,
+                                 float* st, float* stats, void* ws, size_t ws_bytes,
+                                 gfd_stream_t stream);
+
 /* TemporalGNN head (tgn.py:108-111): h_new = GRUCell(h, h0) with PyTorch's
  * gate order (r, z, n) and out = h_new W_out^T + b_out, one kernel (gate
  * pre-activations stay on chip; exact fp32 MFMA products).  h [rows, C] with
