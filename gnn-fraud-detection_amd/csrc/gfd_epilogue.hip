@@ -36,23 +36,34 @@ __global__ void __launch_bounds__(kEB) k_col_stats(
     double* __restrict__ part) {
   __shared__ double sa[kEB], sb[kEB];
   const int c = threadIdx.x & (kC - 1), r0 = threadIdx.x >> 6;
-  double a = 0.0, b = 0.0;
   const float keep = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
-  for (int64_t r = blockIdx.x * 4 + r0; r < N; r += int64_t(gridDim.x) * 4) {
+  // four rows' loads in flight per thread (four accumulator pairs, combined in
+  // a fixed order: the sums stay deterministic)
+  double aa[4] = {0.0, 0.0, 0.0, 0.0}, bb[4] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t stride = int64_t(gridDim.x) * 4;
+  auto row = [&](int64_t r, int u) {
     const float v = y[r * kC + c];
     if (mode == 0) {
-      a += v;
-      b += double(v) * v;
+      aa[u] += v;
+      bb[u] += double(v) * v;
     } else {
       const float xh = (v - mean[c]) * invstd[c];
       const float z = xh * gamma[c] + beta[c];
       float g = gout[r * kC + c];
       if (p > 0.f) g = dropout_keep(seed, uint32_t(r * kC + c), 0, p) ? g * keep : 0.f;
       if (mode == 1) g = z > 0.f ? g : 0.f;
-      a += g;
-      b += double(g) * xh;
+      aa[u] += g;
+      bb[u] += double(g) * xh;
     }
+  };
+  int64_t r = blockIdx.x * 4 + r0;
+  for (; r + 3 * stride < N; r += 4 * stride) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) row(r + u * stride, u);
   }
+  for (; r < N; r += stride) row(r, 0);
+  double a = (aa[0] + aa[1]) + (aa[2] + aa[3]);
+  double b = (bb[0] + bb[1]) + (bb[2] + bb[3]);
   sa[threadIdx.x] = a;
   sb[threadIdx.x] = b;
   __syncthreads();
@@ -73,9 +84,14 @@ __global__ void __launch_bounds__(1024) k_col_final(const double* __restrict__ p
                                                     double* __restrict__ out) {
   __shared__ double red[8][2 * kC];
   const int c = threadIdx.x & (2 * kC - 1), g = threadIdx.x >> 7;
-  double a = 0.0;
-  for (int k = g; k < parts; k += 8) a += part[k * 2 * kC + c];
-  red[g][c] = a;
+  double aa[4] = {0.0, 0.0, 0.0, 0.0};  // four loads in flight, fixed combination order
+  int k = g;
+  for (; k + 24 < parts; k += 32) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) aa[u] += part[(k + 8 * u) * 2 * kC + c];
+  }
+  for (; k < parts; k += 8) aa[0] += part[k * 2 * kC + c];
+  red[g][c] = (aa[0] + aa[1]) + (aa[2] + aa[3]);
   __syncthreads();
   if (threadIdx.x < 2 * kC) {
     double t = 0.0;
