@@ -2,9 +2,11 @@
 // and alpha_src / alpha_dst steps of PyG GATConv.forward; reference call site
 // /root/reference/src/models/gat.py:80, tgn.py:94).
 //
-//   k_wmax        power-of-two scales for W / H and for Wbar = mean_h W_h
-//   k_pack_uv     folded logit vectors U_h = W_h^T a_src[h], V_h = W_h^T a_dst[h]
-//   k_pack_frag*  fp16 hi / lo MFMA B-fragments (head-major, feature-major, Wbar)
+//   k_pack_stage1 block 0: power-of-two scales for W / H and for Wbar =
+//                 mean_h W_h (dev_wmax); other blocks: folded logit vectors
+//                 U_h = W_h^T a_src[h], V_h = W_h^T a_dst[h] (dev_pack_uv)
+//   k_pack_stage2 fp16 hi / lo MFMA B-fragments (head-major, feature-major,
+//                 Wbar in two lane orders) and the [U | V] fragments, by block range
 //   k_logits_s    st[n] = (x_n . U_h, x_n . V_h) on fp32 MFMA (exact fp32 chains),
 //                 plus max |x| for the tile stage's one-scale-per-launch Z rows
 #include "gfd_fwd.h"
@@ -15,8 +17,8 @@ using namespace gfd::fwd;
 namespace {
 
 // One block: max |W| / H and max |Wbar| -> the two power-of-two scales.
-__global__ void __launch_bounds__(1024) k_wmax(const float* __restrict__ W, int F,
-                                               PackHeader* __restrict__ hdr) {
+__device__ __forceinline__ void dev_wmax(const float* __restrict__ W, int F,
+                                         PackHeader* __restrict__ hdr) {
   __shared__ float red[2][1024];
   const int t = threadIdx.x;
   const int n = H * C * F;
@@ -61,9 +63,11 @@ __global__ void __launch_bounds__(1024) k_wmax(const float* __restrict__ W, int 
   }
 }
 
-__global__ void k_pack_uv(const float* __restrict__ W, const float* __restrict__ as,
-                          const float* __restrict__ ad, int F, int Fu, float* __restrict__ uv) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void dev_pack_uv(const float* __restrict__ W,
+                                            const float* __restrict__ as,
+                                            const float* __restrict__ ad, int F, int Fu,
+                                            float* __restrict__ uv, int bid) {
+  int idx = bid * 1024 + threadIdx.x;
   if (idx >= 2 * H * Fu) return;
   int q = idx / Fu, f = idx % Fu;
   int h = q % H;
@@ -76,10 +80,10 @@ __global__ void k_pack_uv(const float* __restrict__ W, const float* __restrict__
 }
 
 // Head-major fragments (k_fused): K position p = h Fp + f; lo' = (v - hi) 2^11.
-__global__ void k_pack_frag(const float* __restrict__ W, int F, int Fp, int KS,
+__device__ __forceinline__ void dev_pack_frag(int bid, const float* __restrict__ W, int F, int Fp, int KS,
                             const PackHeader* __restrict__ hdr, uint4* __restrict__ whi,
                             uint4* __restrict__ wlo) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (s, ct, lane)
+  int idx = bid * 256 + threadIdx.x;  // (s, ct, lane)
   if (idx >= KS * 4 * 64) return;
   int lane = idx & 63, ct = (idx >> 6) & 3, s = idx >> 8;
   int n = ct * 16 + (lane & 15);
@@ -101,10 +105,10 @@ __global__ void k_pack_frag(const float* __restrict__ W, int F, int Fp, int KS,
 // Feature-major fragments (k_stream): K position p = 8 f + h (one 16-B Z
 // store per feature holds all 8 heads), lo = v - hi unscaled (|lo| <= 2^3 for
 // the 2^14-scaled W; fp16 subnormals there cost < 2^-38 of the largest weight).
-__global__ void k_pack_frag_s(const float* __restrict__ W, int F, int KS,
+__device__ __forceinline__ void dev_pack_frag_s(int bid, const float* __restrict__ W, int F, int KS,
                               const PackHeader* __restrict__ hdr, uint4* __restrict__ wsh,
                               uint4* __restrict__ wsl) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (s, ct, lane)
+  int idx = bid * 256 + threadIdx.x;  // (s, ct, lane)
   if (idx >= KS * 4 * 64) return;
   int lane = idx & 63, ct = (idx >> 6) & 3, s = idx >> 8;
   int n = ct * 16 + (lane & 15);
@@ -124,10 +128,10 @@ __global__ void k_pack_frag_s(const float* __restrict__ W, int F, int KS,
 
 // Head-mean fragments (k_lone): B[k = f][n] = mean_h W[h C + n][f] * 2^kb,
 // k-step s covers features 32 s .. 32 s + 31 (8 per lane group), lo unscaled.
-__global__ void k_pack_wbar(const float* __restrict__ W, int F, int KB,
+__device__ __forceinline__ void dev_pack_wbar(int bid, const float* __restrict__ W, int F, int KB,
                             const PackHeader* __restrict__ hdr, uint4* __restrict__ wbh,
                             uint4* __restrict__ wbl) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (s, ct, lane)
+  int idx = bid * 256 + threadIdx.x;  // (s, ct, lane)
   if (idx >= KB * 4 * 64) return;
   int lane = idx & 63, ct = (idx >> 6) & 3, s = idx >> 8;
   int n = ct * 16 + (lane & 15);
@@ -155,10 +159,10 @@ __global__ void k_pack_wbar(const float* __restrict__ W, int F, int KB,
 // group g of k-step t holds, at positions j = 0..7, feature 32 t + 4 g + j
 // (j < 4) or 32 t + 16 + 4 g + j - 4 (j >= 4) -- exactly the features that
 // lane group's fp32 logits loads of k-steps 2 t and 2 t + 1 hold.
-__global__ void k_pack_wbar_perm(const float* __restrict__ W, int F, int KB,
+__device__ __forceinline__ void dev_pack_wbar_perm(int bid, const float* __restrict__ W, int F, int KB,
                                  const PackHeader* __restrict__ hdr, uint4* __restrict__ wph,
                                  uint4* __restrict__ wpl) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (t, ct, lane)
+  int idx = bid * 256 + threadIdx.x;  // (t, ct, lane)
   if (idx >= KB * 4 * 64) return;
   int lane = idx & 63, ct = (idx >> 6) & 3, t = idx >> 8;
   int n = ct * 16 + (lane & 15), g = lane >> 4;
@@ -186,7 +190,7 @@ __global__ void k_pack_wbar_perm(const float* __restrict__ W, int F, int KB,
 // power-of-two scaled by max |uv| -> [2^13, 2^14), f16 hi / lo, in the lane
 // order of k_pack_wbar_perm (fp32 logits pass) and in the plain order of
 // k_pack_wbar (bf16 logits pass).  One block: the max, then the fragments.
-__global__ void __launch_bounds__(256) k_pack_uv_perm(const float* __restrict__ uv, int F, int Fu,
+__device__ __forceinline__ void dev_pack_uv_perm(const float* __restrict__ uv, int F, int Fu,
                                                       int KB, PackHeader* __restrict__ hdr,
                                                       uint4* __restrict__ uph,
                                                       uint4* __restrict__ upl,
@@ -225,6 +229,35 @@ __global__ void __launch_bounds__(256) k_pack_uv_perm(const float* __restrict__ 
     (plain ? ush : uph)[i] = hi.v;
     (plain ? usl : upl)[i] = lo.v;
   }
+}
+
+// The pack in two launches (the seven kernels above as block ranges; round 5:
+// seven small launches cost ~50 us per layer and step):
+//   stage 1 (1024-thread blocks): block 0 the W scales, blocks 1.. U / V
+//   stage 2 (256-thread blocks): fragments (need the scales) and [U | V]
+//           fragments (need U / V), by block range
+struct PackArgs {
+  const float* W; const float* as; const float* ad; int F, Fp, Fu, KS, KB;
+  PackHeader* hdr; float* uv;
+  uint4 *whi, *wlo, *wsh, *wsl, *wbh, *wbl, *wph, *wpl, *uph, *upl, *ush, *usl;
+};
+
+__global__ void __launch_bounds__(1024) k_pack_stage1(PackArgs a) {
+  if (blockIdx.x == 0) dev_wmax(a.W, a.F, a.hdr);
+  else dev_pack_uv(a.W, a.as, a.ad, a.F, a.Fu, a.uv, int(blockIdx.x) - 1);
+}
+
+__global__ void __launch_bounds__(256) k_pack_stage2(PackArgs a) {
+  const int nfr = (a.KS * 4 * 64 + 255) / 256, nwb = (a.KB * 4 * 64 + 255) / 256;
+  int b = blockIdx.x;  // block-uniform ranges
+  if (b < nfr) { dev_pack_frag(b, a.W, a.F, a.Fp, a.KS, a.hdr, a.whi, a.wlo); return; }
+  b -= nfr;
+  if (b < nfr) { dev_pack_frag_s(b, a.W, a.F, a.KS, a.hdr, a.wsh, a.wsl); return; }
+  b -= nfr;
+  if (b < nwb) { dev_pack_wbar(b, a.W, a.F, a.KB, a.hdr, a.wbh, a.wbl); return; }
+  b -= nwb;
+  if (b < nwb) { dev_pack_wbar_perm(b, a.W, a.F, a.KB, a.hdr, a.wph, a.wpl); return; }
+  dev_pack_uv_perm(a.uv, a.F, a.Fu, a.KB, a.hdr, a.uph, a.upl, a.ush, a.usl);
 }
 
 // ---------------------------------------------------------------------------
@@ -392,35 +425,19 @@ gfd_status gfd_gat_pack_weights(const float* weight, const float* att_src, const
   PackLayout L = pack_layout(F);
   char* p = static_cast<char*>(packed);
   PackHeader* hdr = reinterpret_cast<PackHeader*>(p + L.hdr_off);
-  k_wmax<<<1, 1024, 0, stream>>>(weight, F, hdr);
-  GFD_LAUNCH_CHECK();
+  PackArgs a{weight, att_src, att_dst, F, L.Fp, L.Fu, L.KS, L.KB, hdr,
+              reinterpret_cast<float*>(p + L.uv_off),
+              reinterpret_cast<uint4*>(p + L.whi_off), reinterpret_cast<uint4*>(p + L.wlo_off),
+              reinterpret_cast<uint4*>(p + L.wsh_off), reinterpret_cast<uint4*>(p + L.wsl_off),
+              reinterpret_cast<uint4*>(p + L.wbh_off), reinterpret_cast<uint4*>(p + L.wbl_off),
+              reinterpret_cast<uint4*>(p + L.wph_off), reinterpret_cast<uint4*>(p + L.wpl_off),
+              reinterpret_cast<uint4*>(p + L.uph_off), reinterpret_cast<uint4*>(p + L.upl_off),
+              reinterpret_cast<uint4*>(p + L.ush_off), reinterpret_cast<uint4*>(p + L.usl_off)};
   const int n_uv = 2 * H * L.Fu;
-  k_pack_uv<<<(n_uv + 255) / 256, 256, 0, stream>>>(weight, att_src, att_dst, F, L.Fu,
-                                                    reinterpret_cast<float*>(p + L.uv_off));
+  k_pack_stage1<<<1 + (n_uv + 1023) / 1024, 1024, 0, stream>>>(a);
   GFD_LAUNCH_CHECK();
-  const int n_fr = L.KS * 4 * 64;
-  k_pack_frag<<<(n_fr + 255) / 256, 256, 0, stream>>>(weight, F, L.Fp, L.KS, hdr,
-                                                      reinterpret_cast<uint4*>(p + L.whi_off),
-                                                      reinterpret_cast<uint4*>(p + L.wlo_off));
-  GFD_LAUNCH_CHECK();
-  k_pack_frag_s<<<(n_fr + 255) / 256, 256, 0, stream>>>(weight, F, L.KS, hdr,
-                                                        reinterpret_cast<uint4*>(p + L.wsh_off),
-                                                        reinterpret_cast<uint4*>(p + L.wsl_off));
-  GFD_LAUNCH_CHECK();
-  const int n_wb = L.KB * 4 * 64;
-  k_pack_wbar<<<(n_wb + 255) / 256, 256, 0, stream>>>(weight, F, L.KB, hdr,
-                                                      reinterpret_cast<uint4*>(p + L.wbh_off),
-                                                      reinterpret_cast<uint4*>(p + L.wbl_off));
-  GFD_LAUNCH_CHECK();
-  k_pack_wbar_perm<<<(n_wb + 255) / 256, 256, 0, stream>>>(
-      weight, F, L.KB, hdr, reinterpret_cast<uint4*>(p + L.wph_off),
-      reinterpret_cast<uint4*>(p + L.wpl_off));
-  GFD_LAUNCH_CHECK();
-  k_pack_uv_perm<<<1, 256, 0, stream>>>(reinterpret_cast<const float*>(p + L.uv_off), F, L.Fu,
-                                        L.KB, hdr, reinterpret_cast<uint4*>(p + L.uph_off),
-                                        reinterpret_cast<uint4*>(p + L.upl_off),
-                                        reinterpret_cast<uint4*>(p + L.ush_off),
-                                        reinterpret_cast<uint4*>(p + L.usl_off));
+  const int nfr = (L.KS * 4 * 64 + 255) / 256, nwb = (L.KB * 4 * 64 + 255) / 256;
+  k_pack_stage2<<<2 * nfr + 2 * nwb + 1, 256, 0, stream>>>(a);
   GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
