@@ -123,10 +123,15 @@ def test_c2_full_size_train_step_at_adam_updated_weights(elliptic):
     crit(logits[md].squeeze(1), yld).backward()
     torch.cuda.synchronize()
 
+    pre = {}  # the fp64 forward's pre-ReLU values (BatchNorm outputs) per layer
+
     def oracle(dtype):
         ref = GATRef(165, 64, 1, num_layers=3, dropout=0.0).train()
         ref.load_state_dict(sd, strict=True)
         ref = ref.to(dtype)
+        if dtype == torch.float64:
+            for i, bn in enumerate(ref.batch_norms):
+                bn.register_forward_hook(lambda mod, inp, out, i=i: pre.__setitem__(i, out.detach()))
         xr = torch.from_numpy(elliptic["x"]).to(dtype).requires_grad_(True)
         rlogits = ref(xr, torch.from_numpy(elliptic["edge_index"]))
         torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([50.0], dtype=dtype))(
@@ -141,19 +146,38 @@ def test_c2_full_size_train_step_at_adam_updated_weights(elliptic):
     got = {"x": x.grad.detach().cpu().double()}
     got.update({n: q.grad.detach().cpu().double() for n, q in g.named_parameters()
                 if not n.endswith("lin_dst.weight")})
-    report = []
+    # grad_x rows near a ReLU boundary: a pre-activation within 1e-5 of zero in
+    # the fp64 forward can land on the other side of zero in any fp32 dataflow
+    # (the device's or the fp32 oracle's), which masks that channel's gradient
+    # for the node and every node within three hops of it (found at these
+    # weights: one node, pre-ReLU 1.5e-7, 12 % of max |grad_x| on its row --
+    # scripts/diag_c2_test_weights.py).  Those rows are left out of the grad_x
+    # comparison; they must stay a small set.
+    ei = torch.from_numpy(elliptic["edge_index"])
+    near = torch.zeros(ei.max().item() + 1, dtype=torch.bool)
+    for v in pre.values():
+        near |= (v.abs() < 1e-5).any(1)
+    for _ in range(3):
+        near[ei[0][near[ei[1]]]] = True
+        near[ei[1][near[ei[0]]]] = True
+    assert near.float().mean().item() < 0.01, f"{near.sum().item()} rows near a ReLU boundary"
+    report = [f"grad_x rows within 3 hops of a |pre-ReLU| < 1e-5 value: {near.sum().item()}"]
     for name, a in got.items():
         ref = r64[name]
+        if name == "x":
+            a, ref, r32x = a[~near], ref[~near], r32[name][~near]
+        else:
+            r32x = r32[name]
         scale = ref.abs().max().item()
         bound = 2e-4 * scale + (0.0 if name == "x" else 1e-5)
         err = (a - ref).abs().max().item()
-        err32 = (r32[name] - ref).abs().max().item()
+        err32 = (r32x - ref).abs().max().item()
         report.append(f"{name}: err {err:.2e} bound {bound:.2e} fp32-oracle err {err32:.2e}")
         # within the bound, or (ill-conditioned sums: BatchNorm's backward over
         # 203,769 rows cancels) at most half the error of the reference's own
         # fp32 dataflow against fp64
         assert err <= bound or err <= 0.5 * err32, "\n".join(report)
-    assert len(report) >= 16
+    assert len(report) >= 17
 
 
 def test_c3_full_size_49_snapshots_match_oracle(elliptic, golden):
