@@ -149,10 +149,11 @@ def test_c2_full_size_train_step_at_adam_updated_weights(elliptic):
     # grad_x rows near a ReLU boundary: a pre-activation within 1e-5 of zero in
     # the fp64 forward can land on the other side of zero in any fp32 dataflow
     # (the device's or the fp32 oracle's), which masks that channel's gradient
-    # for the node and every node within three hops of it (found at these
-    # weights: one node, pre-ReLU 1.5e-7, 12 % of max |grad_x| on its row --
-    # scripts/diag_c2_test_weights.py).  Those rows are left out of the grad_x
-    # comparison; they must stay a small set.
+    # for the node and, through the layers, nodes up to three hops away (found
+    # at these weights: one row at 12 % of max |grad_x|, next to a layer-2
+    # pre-ReLU value of 1.5e-7 -- scripts/diag_c2_test_weights.py).  So grad_x
+    # is checked row by row: a row passes as every gradient does below, and the
+    # few rows that do not must all lie within three hops of such a value.
     ei = torch.from_numpy(elliptic["edge_index"])
     near = torch.zeros(ei.max().item() + 1, dtype=torch.bool)
     for v in pre.values():
@@ -160,24 +161,27 @@ def test_c2_full_size_train_step_at_adam_updated_weights(elliptic):
     for _ in range(3):
         near[ei[0][near[ei[1]]]] = True
         near[ei[1][near[ei[0]]]] = True
-    assert near.float().mean().item() < 0.01, f"{near.sum().item()} rows near a ReLU boundary"
-    report = [f"grad_x rows within 3 hops of a |pre-ReLU| < 1e-5 value: {near.sum().item()}"]
+    report = []
     for name, a in got.items():
         ref = r64[name]
-        if name == "x":
-            a, ref, r32x = a[~near], ref[~near], r32[name][~near]
-        else:
-            r32x = r32[name]
         scale = ref.abs().max().item()
         bound = 2e-4 * scale + (0.0 if name == "x" else 1e-5)
+        if name == "x":
+            err_r = (a - ref).abs().max(1).values
+            err32_r = (r32[name] - ref).abs().max(1).values
+            bad = ~((err_r <= bound) | (err_r <= 0.5 * err32_r.max()))
+            report.append(f"x: {int(bad.sum())} rows outside the bound, all near a ReLU "
+                          f"boundary: {bool(near[bad].all())}; worst {err_r.max():.2e}")
+            assert int(bad.sum()) <= 20 and bool(near[bad].all()), "\n".join(report)
+            continue
         err = (a - ref).abs().max().item()
-        err32 = (r32x - ref).abs().max().item()
+        err32 = (r32[name] - ref).abs().max().item()
         report.append(f"{name}: err {err:.2e} bound {bound:.2e} fp32-oracle err {err32:.2e}")
         # within the bound, or (ill-conditioned sums: BatchNorm's backward over
         # 203,769 rows cancels) at most half the error of the reference's own
         # fp32 dataflow against fp64
         assert err <= bound or err <= 0.5 * err32, "\n".join(report)
-    assert len(report) >= 17
+    assert len(report) >= 16
 
 
 def test_c3_full_size_49_snapshots_match_oracle(elliptic, golden):
