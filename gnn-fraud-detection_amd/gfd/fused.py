@@ -67,18 +67,22 @@ def head_foldable(head, width: int, conv=None) -> bool:
 def eval_weights(conv, bn, device) -> Tuple[torch.Tensor, torch.Tensor]:
     """(packed weights, BatchNorm scale | shift) of an inference layer, rebuilt
     only when a tensor they derive from changed: the cache on ``conv`` holds
-    each source tensor and its version counter, so a replaced parameter (a new
-    object) or an in-place update (optimizer step, load_state_dict) rebuilds
-    it, while evaluation over many batches (evaluate.py:73-98) packs once."""
+    each source tensor, its version counter and storage address, so a replaced
+    parameter (a new object), an in-place update (optimizer step,
+    load_state_dict) or new storage (``.to(device)``) rebuilds it, while
+    evaluation over many batches (evaluate.py:73-98) packs once."""
     srcs = [conv.lin_src.weight, conv.att_src, conv.att_dst]
     if bn is not None:
         srcs += [bn.running_mean, bn.running_var]
         if bn.affine:
             srcs += [bn.weight, bn.bias]
-    key = [(t, t._version) for t in srcs] + [bn.eps if bn is not None else None, bn]
+    # (object, version, storage address): a module moved to another device or
+    # given new .data keeps its parameter objects but not their storage
+    key = [(t, t._version, t.data_ptr()) for t in srcs] + [bn.eps if bn is not None else None,
+                                                             bn, str(device)]
     c = conv.__dict__.get("_gfd_eval")
     if c is not None and len(c[0]) == len(key) and all(
-            (a[0] is b[0] and a[1] == b[1]) if isinstance(a, tuple) else a is b or a == b
+            (a[0] is b[0] and a[1:] == b[1:]) if isinstance(a, tuple) else a is b or a == b
             for a, b in zip(c[0], key)):
         return c[1], c[2]
     W = conv.lin_src.weight.detach().contiguous()
