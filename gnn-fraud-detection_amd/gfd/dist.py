@@ -915,3 +915,169 @@ def all_reduce_grads(params, group=None) -> None:
         n = p.grad.numel()
         p.grad.copy_(flat[off:off + n].view_as(p.grad))
         off += n
+
+
+# ---------------------------------------------------------------------------
+# Sharded training of the whole model (train.py:115-143 on destination shards)
+#
+# Layer 0 runs on the rank's LocalGraph with x gathered into the local order
+# (``LocalGraph.rows``: x is a constant input, resident on every rank).  A
+# hidden layer's input is the previous layer's output, which exists only on
+# each node's owner: ``halo_rows`` brings the halo rows in (the HaloPlan of the
+# shard: one all-to-all) and, in the backward, sends their gradients back to
+# the owners (the reverse all-to-all), where they are added to the own rows'
+# gradients -- so a hidden layer's grad_x crosses ranks exactly as its forward
+# input did.  BatchNorm takes batch statistics over ALL nodes
+# (``sharded_batch_norm``: the per-channel sums are all-reduced, forward and
+# backward).  The loss is the reference's mean over labelled nodes, taken as
+# each rank's sum over its own labelled nodes divided by the global count, so
+# the ranks' losses add up to it; ``all_reduce_grads`` then sums the partial
+# parameter gradients.
+
+
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group) -> None:
+    """all_to_all_single of rows; device tensors over gloo (the one-GPU
+    multi-process rehearsals) are staged through host memory."""
+    import torch.distributed as dist
+    if inp.is_cuda and dist.get_backend(group) == "gloo":
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits,
+                               input_split_sizes=in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
+                               input_split_sizes=in_splits, group=group)
+
+
+def _all_reduce(t: torch.Tensor, group) -> None:
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+
+
+class _HaloRows(torch.autograd.Function):
+    """own rows [n_own, C] -> local rows [n_own + n_halo, C] (LocalGraph order);
+    backward: the halo rows' gradients back to their owners."""
+
+    @staticmethod
+    def forward(ctx, h_own, plan, lo, group):
+        send_idx = plan.send_rows.to(h_own.device).long() - lo
+        send = h_own.index_select(0, send_idx).contiguous()
+        recv = h_own.new_empty((int(plan.recv_rows.numel()), h_own.size(1)))
+        _a2a(recv, send, plan.recv_counts, plan.send_counts, group)
+        ctx.plan, ctx.group, ctx.n_own = plan, group, h_own.size(0)
+        ctx.save_for_backward(send_idx)
+        return torch.cat([h_own, recv], 0)
+
+    @staticmethod
+    def backward(ctx, g_local):
+        (send_idx,) = ctx.saved_tensors
+        plan, n_own = ctx.plan, ctx.n_own
+        g_own = g_local[:n_own].clone()
+        g_halo = g_local[n_own:].contiguous()
+        back = g_local.new_empty((int(send_idx.numel()), g_local.size(1)))
+        _a2a(back, g_halo, plan.send_counts, plan.recv_counts, ctx.group)
+        # one peer at a time: within a peer's list every own row appears once,
+        # so each index_add is free of duplicate-index races and the peers are
+        # added in a fixed order (deterministic)
+        off = 0
+        for c in plan.send_counts:
+            if c:
+                g_own.index_add_(0, send_idx[off:off + c], back[off:off + c])
+            off += c
+        return g_own, None, None, None
+
+
+def halo_rows(h_own: torch.Tensor, plan: HaloPlan, lo: int, group=None) -> torch.Tensor:
+    """[n_own + n_halo, C]: this rank's rows of a per-node tensor followed by its
+    halo rows (ascending node id, as LocalGraph orders them), differentiable."""
+    return _HaloRows.apply(h_own, plan, int(lo), group)
+
+
+class _ShardedBN(torch.autograd.Function):
+    """Training-mode BatchNorm1d over rows spread across ranks."""
+
+    @staticmethod
+    def forward(ctx, y, weight, bias, n_total, eps, group):
+        yd = y.double()
+        sums = torch.cat([yd.sum(0), (yd * yd).sum(0)])
+        _all_reduce(sums, group)
+        C = y.size(1)
+        mean = sums[:C] / n_total
+        var = (sums[C:] / n_total - mean * mean).clamp_min(0.0)
+        invstd = (var + eps).rsqrt()
+        xhat = ((yd - mean) * invstd).to(y.dtype)
+        ctx.save_for_backward(xhat, weight, invstd.to(y.dtype))
+        ctx.n_total, ctx.group = n_total, group
+        mean, var = mean.to(y.dtype), var.to(y.dtype)
+        ctx.mark_non_differentiable(mean, var)
+        return xhat * weight + bias, mean, var
+
+    @staticmethod
+    def backward(ctx, g, _gm, _gv):
+        xhat, weight, invstd = ctx.saved_tensors
+        gd, xd = g.double(), xhat.double()
+        sums = torch.cat([gd.sum(0), (gd * xd).sum(0)])
+        grad_bias_part = sums[:g.size(1)].to(g.dtype).clone()     # this rank's partial sums
+        grad_weight_part = sums[g.size(1):].to(g.dtype).clone()
+        _all_reduce(sums, ctx.group)
+        C, n = g.size(1), ctx.n_total
+        dy = (weight.double() * invstd.double() / n) * (n * gd - sums[:C] - xd * sums[C:])
+        return dy.to(g.dtype), grad_weight_part, grad_bias_part, None, None, None
+
+
+def sharded_batch_norm(y: torch.Tensor, bn: torch.nn.BatchNorm1d, n_total: int,
+                       group=None) -> torch.Tensor:
+    """``bn(y)`` in training mode with the batch statistics of all ranks' rows
+    (``n_total`` rows in all); the running statistics are updated as
+    torch.nn.BatchNorm1d does (unbiased variance), identically on every rank.
+    The weight / bias gradients are this rank's partial sums (all_reduce_grads)."""
+    out, mean, var = _ShardedBN.apply(y, bn.weight, bn.bias, float(n_total), float(bn.eps), group)
+    if bn.track_running_stats and bn.running_mean is not None:
+        with torch.no_grad():
+            bn.num_batches_tracked += 1
+            m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+            rdt = bn.running_mean.dtype
+            unbiased = var.to(rdt) * (n_total / max(n_total - 1, 1))
+            bn.running_mean.mul_(1 - m).add_(m * mean.to(rdt))
+            bn.running_var.mul_(1 - m).add_(m * unbiased)
+    return out
+
+
+def gat_conv_on_local(conv, x_local: torch.Tensor, local: LocalGraph, training: bool):
+    """One GATConv on the LocalGraph's rows (the HIP kernels); own rows returned."""
+    from .nn import gat_conv
+    out = gat_conv(x_local, local.graph, conv.lin_src.weight, conv.att_src, conv.att_dst,
+                   conv.bias, conv.negative_slope, conv.dropout, training)
+    return out[:local.n_dst]
+
+
+def gat_forward_sharded_train(model, x: torch.Tensor, local: LocalGraph, plan: HaloPlan,
+                              n_total: int, conv_fn=None, group=None) -> torch.Tensor:
+    """The reference GAT's training forward (gat.py:60-96) for this rank's own
+    nodes: [n_own, out] logits.  ``plan``: HaloPlan.create of the shard
+    (hidden-layer halo exchange); ``n_total``: nodes over all ranks (BatchNorm);
+    ``conv_fn(conv, x_local, local, training)``: the GATConv on local rows
+    (default the HIP kernels; the CPU tests pass the oracle's arithmetic).
+    Dropout masks are drawn per rank (equally distributed, not the
+    single-process masks)."""
+    import torch.nn.functional as F
+    from .models import _head
+    conv_fn = conv_fn or gat_conv_on_local
+    lo = local.lo
+    h_own = None
+    for li, conv in enumerate(model.gat_layers):
+        x_local = local.rows(x) if li == 0 else halo_rows(h_own, plan, lo, group)
+        y = conv_fn(conv, x_local, local, model.training)
+        if model.batch_norms is not None:
+            bn = model.batch_norms[li]
+            # eval: the running statistics, identical on every rank
+            y = sharded_batch_norm(y, bn, n_total, group) if model.training else bn(y)
+        y = F.dropout(F.relu(y), p=model.dropout, training=model.training)
+        h_prev = x_local[:local.n_dst]
+        h_own = h_prev + y if (model.residual and h_prev.size(-1) == y.size(-1)) else y
+    return _head(model.out, h_own)

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from _util import assert_close_scaled, csr_cpu
-from test_dist_cpu import _problem, _store_path, N, H, C
+from test_dist_cpu import _problem, _store_path, N, F, H, C
 from gfd import dist as gdist
 from gfd.graph import CSRGraph
 from oracle import gatconv_ref as ref
@@ -107,3 +107,106 @@ def test_local_graph_structure():
         # constant x: gathered once per version
         a = lg.rows(x)
         assert lg.rows(x) is a and torch.equal(a, x[nodes])
+
+
+# ---------------------------------------------------------------------------
+# The whole model (gat.py:60-96, train.py:115-143): three GATConv layers with
+# BatchNorm, ReLU and the residual, sharded by destination.  Hidden layers
+# receive their halo rows through gdist.halo_rows (and send the halo rows'
+# gradients back to the owners), BatchNorm takes all ranks' rows
+# (gdist.sharded_batch_norm), and the loss is each rank's share of the
+# labelled-node mean.  fp64 throughout, so the comparison is tight.
+
+LAYERS = 3
+
+
+def _model_problem():
+    ei, x, *_ = _problem()
+    g = torch.Generator().manual_seed(11)
+    y = (torch.rand(N, generator=g) < 0.2).double()
+    mask = torch.rand(N, generator=g) < 0.6
+    torch.manual_seed(3)
+    from gfd.models import GAT
+    model = GAT(F, C, 1, num_layers=LAYERS, dropout=0.0).double().train()
+    with torch.no_grad():   # non-trivial BN affine parameters
+        for bn in model.batch_norms:
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+    return ei, x.double(), y, mask, model
+
+
+def _oracle_conv(conv, x_local, lg, training):
+    return ref.gatconv_forward(x_local, _local_coo(lg), conv.lin_src.weight, conv.att_src,
+                               conv.att_dst, conv.bias, heads=H)[:lg.n_dst]
+
+
+def _reference_step(ei, x, y, mask, model):
+    import torch.nn.functional as Fn
+    h = x
+    for li, conv in enumerate(model.gat_layers):
+        z = ref.gatconv_forward(h, ei, conv.lin_src.weight, conv.att_src, conv.att_dst,
+                                conv.bias, heads=H)
+        z = Fn.relu(model.batch_norms[li](z))
+        h = h + z if h.size(-1) == z.size(-1) else z
+    logits = model.out(h).squeeze(-1)
+    loss = Fn.binary_cross_entropy_with_logits(logits[mask], y[mask])
+    loss.backward()
+    return loss.item()
+
+
+def _model_rank(rank, world, path, balance, q):
+    import torch.nn.functional as Fn
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
+    try:
+        ei, x, y, mask, model = _model_problem()
+        g = _graph_cpu(ei)
+        spec = gdist.ShardSpec(g.rowptr.long(), rank, world, balance)
+        lo, hi = spec.dst_lo, spec.dst_hi
+        lg = gdist.local_graph(g, lo, hi)
+        rp = g.rowptr.long()
+        plan = gdist.HaloPlan.create(g.col[int(rp[lo]):int(rp[hi])], spec)
+        logits = gdist.gat_forward_sharded_train(model, x, lg, plan, N,
+                                                 conv_fn=_oracle_conv).squeeze(-1)
+        m = mask[lo:hi]
+        part = Fn.binary_cross_entropy_with_logits(logits[m], y[lo:hi][m], reduction="sum")
+        loss = part / int(mask.sum())
+        loss.backward()
+        gdist.all_reduce_grads(list(model.parameters()))
+        tot = loss.detach().clone()
+        dist.all_reduce(tot)
+        if rank == 0:
+            q.put(({k: p.grad.numpy() for k, p in model.named_parameters()},
+                   {k: b.numpy() for k, b in model.named_buffers()}, tot.item(),
+                   plan.recv_rows.numel()))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,balance", [(2, "messages"), (3, "cost")])
+def test_sharded_model_train_step_matches_single_process(world, balance):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = _store_path()
+    procs = [ctx.Process(target=_model_rank, args=(r, world, path, balance, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    grads, bufs, loss, n_halo = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ei, x, y, mask, model = _model_problem()
+    want_loss = _reference_step(ei, x, y, mask, model)
+    assert abs(loss - want_loss) <= 1e-12 * max(1.0, abs(want_loss))
+    assert n_halo > 0   # the hidden layers really exchanged rows
+    for k, p in model.named_parameters():
+        # atol: a GATConv bias feeding a train-mode BatchNorm has a zero gradient
+        assert_close_scaled(torch.from_numpy(grads[k]), p.grad, rtol=1e-10, atol=1e-13,
+                            what=f"sharded model grad {k}, world {world} ({balance})")
+    for k, b in model.named_buffers():
+        if b.dtype.is_floating_point:
+            assert_close_scaled(torch.from_numpy(bufs[k]), b, rtol=1e-10,
+                                what=f"BN buffer {k}, world {world}")
+        else:
+            assert int(bufs[k]) == int(b)
