@@ -512,9 +512,12 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// EPI = false: an instance without the epilogue (e.ab == NULL at run time).
+template <bool EPI = true>
 __device__ __forceinline__ float epi_store_value(float v, float bias_n, int n, int64_t row,
                                                  const Epi& e) {
   float y = v + bias_n;
+  if constexpr (!EPI) return y;
   if (e.ab) {
     y = fmaf(y, e.ab[n], e.ab[C + n]);
     if (e.relu) y = fmaxf(y, 0.f);

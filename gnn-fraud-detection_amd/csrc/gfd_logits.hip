@@ -61,7 +61,7 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <typename XT, int KS, bool HEAD, bool A16>
+template <typename XT, int KS, bool HEAD, bool A16, bool EPI>
 __global__ void __launch_bounds__(kLLWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_logits_lone(
     const typename XT::T* __restrict__ x, int64_t rows, int F, int64_t ldx,
@@ -379,7 +379,7 @@ k_logits_lone(
           float d = 0.f;
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
-            d = fmaf(epi_store_value(o[ct][q] * uq, BH[0][ct * 16 + rl], ct * 16 + rl, orow, ep),
+            d = fmaf(epi_store_value<EPI>(o[ct][q] * uq, BH[0][ct * 16 + rl], ct * 16 + rl, orow, ep),
                      BH[1][ct * 16 + rl], d);
           d = row16_sum(d);
           if (rl == 0) ep.hout[orow] = d + (ep.hb ? ep.hb[0] : 0.f);
@@ -405,7 +405,7 @@ k_logits_lone(
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           T[(4 * g + q) * kTP + n] =
-              lq[q] ? epi_store_value(o[ct][q] * uq[q], bn, n, t * 16 + 4 * g + q, ep) : 0.f;
+              lq[q] ? epi_store_value<EPI>(o[ct][q] * uq[q], bn, n, t * 16 + 4 * g + q, ep) : 0.f;
       }
       lds_order();
 #pragma unroll
@@ -444,14 +444,15 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
   const uintptr_t xa = reinterpret_cast<uintptr_t>(x);
   const bool a16 = xa % 16 == 0 && (ldx * XT::kBytes) % 16 == 0;
   const bool k11 = F <= 176;
-  auto kern = a16 ? (ep.hout ? (k11 ? &k_logits_lone<XT, 11, true, true>
-                                    : &k_logits_lone<XT, 12, true, true>)
-                             : (k11 ? &k_logits_lone<XT, 11, false, true>
-                                    : &k_logits_lone<XT, 12, false, true>))
-                  : (ep.hout ? (k11 ? &k_logits_lone<XT, 11, true, false>
-                                    : &k_logits_lone<XT, 12, true, false>)
-                             : (k11 ? &k_logits_lone<XT, 11, false, false>
-                                    : &k_logits_lone<XT, 12, false, false>));
+  // the epilogue (BN affine / ReLU / residual) and the folded head in their
+  // own instances: the plain pass carries none of their code
+  const bool epi = ep.ab != nullptr;
+#define GFD_LL(KS, HD, A) (epi ? &k_logits_lone<XT, KS, HD, A, true> : &k_logits_lone<XT, KS, HD, A, false>)
+  auto kern = a16 ? (ep.hout ? (k11 ? GFD_LL(11, true, true) : GFD_LL(12, true, true))
+                             : (k11 ? GFD_LL(11, false, true) : GFD_LL(12, false, true)))
+                  : (ep.hout ? (k11 ? GFD_LL(11, true, false) : GFD_LL(12, true, false))
+                             : (k11 ? GFD_LL(11, false, false) : GFD_LL(12, false, false)));
+#undef GFD_LL
   const size_t smem = sizeof(uint4) * 2 * kLKB * 5 * 64 + sizeof(float) * 2 * C +
                       sizeof(float) * kLLWaves * 16 * kTP;
   if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;

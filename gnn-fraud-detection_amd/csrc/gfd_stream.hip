@@ -47,6 +47,12 @@ using namespace gfd::fwd;
 
 namespace {
 
+// The epilogue (BN affine / ReLU / residual, gfd.fused) and the folded model
+// head are compiled into EPI instances only: the plain layer's tile loop then
+// carries none of their code (C4 -0.2 ms against one instance with run-time
+// checks: profiles/r5z_epi_instances.txt)
+#define GFD_HOUT(ep) (EPI && ep.hout)
+
 constexpr int kSWaves = 8;
 // Light slots: message weights broadcast through LDS (fma_k_lds: 2 broadcast
 // reads per message instead of 8 v_readlane; the light kernel's VALU count
@@ -420,7 +426,7 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
   }
 }
 
-template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
+template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT, bool EPI>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t num_dst, const int4* __restrict__ desc,
@@ -539,13 +545,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const int* rid = rid0 + tpar * kTile;
     const f32x4 sum = acc + red0[(tpar * 4 + ct) * 64 + lane];
     const int n = ct * 16 + (lane & 15);
-    if (ep.hout) {  // kernel-uniform: the head's dot over this wave's 16 columns
+    if (GFD_HOUT(ep)) {  // kernel-uniform: the head's dot over this wave's 16 columns
       const float w = ep.hw[n];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = (lane >> 4) * 4 + q;
         const int ri = rid[r];
-        const float v = ri >= 0 ? epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep) * w
+        const float v = ri >= 0 ? epi_store_value<EPI>(sum[q] * (rsc[r] * wu), bcol, n, ri, ep) * w
                                 : 0.f;
         const float d = row16_sum(v);  // lanes 16 k .. 16 k + 15 hold row 4 k + q
         if ((lane & 15) == 0) {
@@ -559,7 +565,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     for (int q = 0; q < 4; ++q) {
       const int r = (lane >> 4) * 4 + q;
       const int ri = rid[r];
-      if (ri >= 0) out[int64_t(ri) * ep.ldo + n] = epi_store_value(sum[q] * (rsc[r] * wu), bcol, n, ri, ep);
+      if (ri >= 0) out[int64_t(ri) * ep.ldo + n] = epi_store_value<EPI>(sum[q] * (rsc[r] * wu), bcol, n, ri, ep);
     }
   };
   // the head's outputs of a finished tile: the four column tiles' partials in
@@ -672,7 +678,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #endif
 
     // ---- tile v + 1: aggregate its rows into Z ----
-    if (ep.hout && v > 0) head_out(pn);  // tile v - 1 (its partials: before barrier 1)
+    if (GFD_HOUT(ep) && v > 0) head_out(pn);  // tile v - 1 (its partials: before barrier 1)
     if (more) aggregate(pn);
 #ifdef GFD_PROF
     const unsigned long long ts3 = __builtin_amdgcn_s_memtime();
@@ -697,7 +703,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #undef GFD_ROW
 #undef GFD_ISSUE
   if (!kh) reduce_store(acc_prev, int((nv - 1) & 1));  // last tile
-  if (ep.hout) {  // kernel-uniform
+  if (GFD_HOUT(ep)) {  // kernel-uniform
     __syncthreads();
     head_out(int((nv - 1) & 1));
   }
@@ -713,7 +719,13 @@ size_t stream_smem(int Fp, int lo) {
 template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
-  auto kern = &k_stream<XT, KF, KHM, LO, EXACT, LIGHT>;
+#ifdef GFD_AB_EPI_ON  // A/B: the epilogue instance for every launch
+  const bool epi = true;
+#else
+  const bool epi = a.ep.ab != nullptr || a.ep.hout != nullptr;
+#endif
+  auto kern = epi ? &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, true>
+                  : &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, false>;
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
   const size_t lds = stream_smem(L.Fp, LO);
   if (L.KS / 2 > KHM || lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;

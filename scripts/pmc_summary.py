@@ -34,7 +34,9 @@ def per_kernel(d):
 
 def stage_of(k):
     if k.startswith("k_stream<"):
-        return "light" if k.rstrip(">").rstrip().endswith("true") else "general"
+        # k_stream<XT, KF, KHM, LO, EXACT, LIGHT, EPI>
+        args = [a.strip() for a in k[k.index("<") + 1:k.rindex(">")].split(",")]
+        return "light" if args[5] == "true" else "general"
     if k.startswith(("k_hub_partial", "k_hub_fin")):
         return "hubs"
     if k.startswith(("k_logits_lone", "k_wmax", "k_pack_")):
