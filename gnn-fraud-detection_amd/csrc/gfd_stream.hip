@@ -181,6 +181,10 @@ template <int KF>
 __device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[kLightMax][KF],
                                           float p, int kmax) {
   static_assert(kLightMax >= 4 && kLightMax <= 7, "light slots: 4 .. 7 messages");
+#ifdef GFD_AB_LIGHT_K6  // A/B: one block for every count (rows past n carry p = 0)
+  fma_k<KF, kLightMax>(z, xv, p);
+  return;
+#endif
   if (kmax <= 2) fma_k<KF, 2>(z, xv, p);
   else if (kmax == 3) fma_k<KF, 3>(z, xv, p);
   else if (kLightMax == 4 || kmax == 4) fma_k<KF, 4>(z, xv, p);
