@@ -174,10 +174,15 @@ def _model_rank(rank, world, path, balance, q):
         gdist.all_reduce_grads(list(model.parameters()))
         tot = loss.detach().clone()
         dist.all_reduce(tot)
+        # eval mode after the step: BatchNorm on the (all-rank) running statistics
+        model.eval()
+        with torch.no_grad():
+            ev = gdist.gat_forward_sharded_train(model, x, lg, plan, N, conv_fn=_oracle_conv)
+        full = gdist.all_gather_v_rows(ev.contiguous(), spec.dst_bounds)
         if rank == 0:
             q.put(({k: p.grad.numpy() for k, p in model.named_parameters()},
                    {k: b.numpy() for k, b in model.named_buffers()}, tot.item(),
-                   plan.recv_rows.numel()))
+                   plan.recv_rows.numel(), full.numpy()))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -192,7 +197,7 @@ def test_sharded_model_train_step_matches_single_process(world, balance):
              for r in range(world)]
     for p in procs:
         p.start()
-    grads, bufs, loss, n_halo = q.get(timeout=180)
+    grads, bufs, loss, n_halo, eval_logits = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -210,3 +215,15 @@ def test_sharded_model_train_step_matches_single_process(world, balance):
                                 what=f"BN buffer {k}, world {world}")
         else:
             assert int(bufs[k]) == int(b)
+    # the eval forward of the updated buffers, sharded vs whole graph
+    model.eval()
+    with torch.no_grad():
+        h = x
+        for li, conv in enumerate(model.gat_layers):
+            z = ref.gatconv_forward(h, ei, conv.lin_src.weight, conv.att_src, conv.att_dst,
+                                    conv.bias, heads=H)
+            z = torch.relu(model.batch_norms[li](z))
+            h = h + z if h.size(-1) == z.size(-1) else z
+        want = model.out(h)
+    assert_close_scaled(torch.from_numpy(eval_logits), want, rtol=1e-10,
+                        what=f"sharded eval logits, world {world}")
