@@ -2085,23 +2085,26 @@ BwdLayout bwd_layout(int64_t N, int64_t M, int F, int64_t hubs, int64_t chunks,
   return L;
 }
 
-// The fused source pass + grad_W' GEMM (k_src_gw), opt-in with GFD_BWD_FUSED=1
-// when grad_x is not requested and F fits it.  Not the default: at C4 it runs
+// The fused source pass + grad_W' GEMM (k_src_gw), opt-in through
+// gfd_gat_bwd_mode (GFD_BWD_FUSED8 / GFD_BWD_FUSED16: the caller's explicit
+// choice -- the library reads no environment) when grad_x is not requested
+// and F fits it.  Not the default: at C4 it runs
 // 23.9 ms against 21.5 ms for k_xmax + k_bwd_src + k_gw.
 // Its scratch (tile costs, their prefix, the slab bounds) follows the compact
 // hub rows in the dh region, which the fused pass does not otherwise use.
 struct FusedPlan {
   int S = 0;  // 0: unfused
-  int NW = 8;  // waves per block (GFD_BWD_FUSED=1: 8, =2: 16)
+  int NW = 8;  // waves per block (GFD_BWD_FUSED8: 8, GFD_BWD_FUSED16: 16)
   int64_t nt = 0;
   size_t scratch = 0, pre_off = 0, bounds_off = 0;
 };
 
-FusedPlan fused_plan(int64_t N, int F, int64_t shubs, bool want_gx) {
+FusedPlan fused_plan(int64_t N, int F, int64_t shubs, bool want_gx, int mode) {
   FusedPlan p;
-  const char* e = getenv("GFD_BWD_FUSED");
-  if (want_gx || !(e && (e[0] == '1' || e[0] == '2')) || (F + 15) / 16 * 16 > kFMaxFu) return p;
-  p.NW = e[0] == '2' ? 16 : 8;
+  if (want_gx || !(mode == GFD_BWD_FUSED8 || mode == GFD_BWD_FUSED16) ||
+      (F + 15) / 16 * 16 > kFMaxFu)
+    return p;
+  p.NW = mode == GFD_BWD_FUSED16 ? 16 : 8;
   int64_t S = (N + 4095) / 4096;
   if (S > cu_count()) S = cu_count();
   if (S < 1) S = 1;
@@ -2193,7 +2196,8 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
                     int64_t M, const float* W, const float* att_src, const float* att_dst,
                     float slope, float dp, uint64_t seed, const float* st, const float* stats,
                     const float* g, float* grad_x, float* grad_W, float* grad_as, float* grad_ad,
-                    float* grad_bias, const uint32_t* xcm, void* ws, hipStream_t stream) {
+                    float* grad_bias, const uint32_t* xcm, int mode, void* ws,
+                    hipStream_t stream) {
   const int64_t hubs = plan ? plan->num_hubs : 0, chunks = plan ? plan->num_chunks : 0;
   const int64_t shubs = src_plan ? src_plan->num_hubs : 0;
   const int64_t schunks = src_plan ? src_plan->num_chunks : 0;
@@ -2240,7 +2244,7 @@ gfd_status bwd_impl(const typename XT::T* x, int64_t N, int F, int64_t ldx, cons
     const gfd_status xs = launch_xmax<XT>(x, N, F, ldx, xvec, amax, kDH, stream);
     if (xs != GFD_OK) return xs;
   }
-  const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr);
+  const FusedPlan fp = fused_plan(N, F, shubs, grad_x != nullptr, mode);
   if (fp.S > 0) {
     // source hubs first: their dh' rows, compact, at the start of the dh region
     if (shubs > 0) {
@@ -2356,16 +2360,19 @@ size_t gfd_gat_bwd_workspace_size(int64_t N, int64_t M, int F, int heads, int ch
   return s.off;
 }
 
-gfd_status gfd_gat_bwd_ex(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
-                       const int32_t* rowptr, const int32_t* col, const gfd_plan* plan,
-                       const int32_t* colptr, const int32_t* csc_dst, const int32_t* csc_eid,
-                       const gfd_plan* src_plan, int64_t M, const float* W, const float* att_src,
-                       const float* att_dst, int heads, int channels, float slope, float dp,
-                       uint64_t seed, const float* st, const float* stats, const float* g,
-                       float* grad_x, float* grad_W, float* grad_as, float* grad_ad,
-                          float* grad_bias, const uint32_t* x_colmax, void* ws, size_t ws_bytes,
-                          gfd_stream_t stream_) {
+gfd_status gfd_gat_bwd_mode(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
+                            const int32_t* rowptr, const int32_t* col, const gfd_plan* plan,
+                            const int32_t* colptr, const int32_t* csc_dst, const int32_t* csc_eid,
+                            const gfd_plan* src_plan, int64_t M, const float* W,
+                            const float* att_src, const float* att_dst, int heads, int channels,
+                            float slope, float dp, uint64_t seed, const float* st,
+                            const float* stats, const float* g, float* grad_x, float* grad_W,
+                            float* grad_as, float* grad_ad, float* grad_bias,
+                            const uint32_t* x_colmax, int mode, void* ws, size_t ws_bytes,
+                            gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
+  if (mode != GFD_BWD_DH && mode != GFD_BWD_FUSED8 && mode != GFD_BWD_FUSED16)
+    return GFD_ERR_ARGUMENT;
   if (heads != H || channels != C || F < 1 || F > 256) return GFD_ERR_UNSUPPORTED;
   if (x_dtype != GFD_DTYPE_F32 && x_dtype != GFD_DTYPE_BF16) return GFD_ERR_ARGUMENT;
   if (N <= 0 || M <= 0 || !xv || !rowptr || !col || !colptr || !csc_dst || !csc_eid || !W ||
@@ -2395,10 +2402,26 @@ gfd_status gfd_gat_bwd_ex(const void* xv, int x_dtype, int64_t N, int F, int64_t
   if (x_dtype == GFD_DTYPE_BF16)
     return bwd_impl<XBF16>(static_cast<const uint16_t*>(xv), N, F, ldx, rowptr, col, plan, colptr,
                     csc_dst, csc_eid, src_plan, M, W, att_src, att_dst, slope, dp, seed, st, stats,
-                    g, grad_x, grad_W, grad_as, grad_ad, grad_bias, x_colmax, ws, stream);
+                    g, grad_x, grad_W, grad_as, grad_ad, grad_bias, x_colmax, mode, ws, stream);
   return bwd_impl<XF32>(static_cast<const float*>(xv), N, F, ldx, rowptr, col, plan, colptr, csc_dst,
                   csc_eid, src_plan, M, W, att_src, att_dst, slope, dp, seed, st, stats, g, grad_x,
-                  grad_W, grad_as, grad_ad, grad_bias, x_colmax, ws, stream);
+                  grad_W, grad_as, grad_ad, grad_bias, x_colmax, mode, ws, stream);
+}
+
+gfd_status gfd_gat_bwd_ex(const void* xv, int x_dtype, int64_t N, int F, int64_t ldx,
+                          const int32_t* rowptr, const int32_t* col, const gfd_plan* plan,
+                          const int32_t* colptr, const int32_t* csc_dst, const int32_t* csc_eid,
+                          const gfd_plan* src_plan, int64_t M, const float* W,
+                          const float* att_src, const float* att_dst, int heads, int channels,
+                          float slope, float dp, uint64_t seed, const float* st,
+                          const float* stats, const float* g, float* grad_x, float* grad_W,
+                          float* grad_as, float* grad_ad, float* grad_bias,
+                          const uint32_t* x_colmax, void* ws, size_t ws_bytes,
+                          gfd_stream_t stream) {
+  return gfd_gat_bwd_mode(xv, x_dtype, N, F, ldx, rowptr, col, plan, colptr, csc_dst, csc_eid,
+                          src_plan, M, W, att_src, att_dst, heads, channels, slope, dp, seed, st,
+                          stats, g, grad_x, grad_W, grad_as, grad_ad, grad_bias, x_colmax,
+                          GFD_BWD_DH, ws, ws_bytes, stream);
 }
 
 

@@ -253,7 +253,7 @@ const char* gfd_status_string(gfd_status s) {
   }
 }
 
-int gfd_abi_version(void) { return 6; }
+int gfd_abi_version(void) { return 7; }
 
 static size_t csr_layout(int64_t E, int64_t N, size_t* sort_tmp_out, size_t* scan_tmp_out) {
   size_t sort_tmp = 0, scan_tmp = 0;

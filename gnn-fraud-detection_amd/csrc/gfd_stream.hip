@@ -54,6 +54,15 @@ namespace {
 #define GFD_HOUT(ep) (EPI && ep.hout)
 
 constexpr int kSWaves = 8;
+// Z tile row pad (halves): 8 gives the A-fragment ds_read_b128 reads a 2-way
+// bank conflict in one of their 16-lane groups, 16 none (scripts/bank_pad.py)
+// fp32 light rows with 64 + Fp / 2 <= F go to the paired-phase kernel (gfd_light.hip)
+#ifndef GFD_LIGHT_PAIR
+#define GFD_LIGHT_PAIR 1
+#endif
+#ifndef GFD_STREAM_ZPAD
+#define GFD_STREAM_ZPAD 8
+#endif
 // Light slots: message weights broadcast through LDS (fma_k_lds: 2 broadcast
 // reads per message instead of 8 v_readlane; the light kernel's VALU count
 // -25 %) -- measured neutral (C4 light 6.34-6.61 vs 6.36-6.51 ms across three
@@ -441,7 +450,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     float* __restrict__ stats, const float* __restrict__ xmax,
     const int64_t* __restrict__ split, int to_end, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) char ssm[];
-  const int ZS = 8 * Fp + 8;                                    // row stride (fp16), 16-B pad
+  const int ZS = 8 * Fp + GFD_STREAM_ZPAD;                      // row stride (fp16)
   const int KH = EXACT ? KHM : Fp / 8;                          // k-steps per K half (<= KHM)
   _Float16* Zh = reinterpret_cast<_Float16*>(ssm);              // [16][ZS]
   _Float16* Zl = Zh + kTile * ZS;                               // [16][ZS]
@@ -714,7 +723,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 }
 
 size_t stream_smem(int Fp, int lo) {
-  return sizeof(_Float16) * 2 * kTile * (8 * Fp + 8) + sizeof(f32x4) * 2 * 4 * 64 +
+  return sizeof(_Float16) * 2 * kTile * (8 * Fp + GFD_STREAM_ZPAD) + sizeof(f32x4) * 2 * 4 * 64 +
          sizeof(SlotRing) * 2 * kTile + sizeof(float) * 4 * kTile +
          sizeof(uint4) * kSWaves * lo * 64 + sizeof(float) * 2 * 4 * kTile +
          sizeof(int) * 2 * kTile;
@@ -788,6 +797,9 @@ gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols || !p.class_split) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
+#if GFD_LIGHT_PAIR
+  if (light_pair_supported(a, L)) return launch_light_pair(a, L, to_end, stream);
+#endif
   return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, stream)
                                  : launch_stream_x<XF32, true>(a, L, to_end, stream);
 }

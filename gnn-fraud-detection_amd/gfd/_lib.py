@@ -132,6 +132,9 @@ SIGNATURES = {
     "gfd_gat_bwd_ex": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, PLAN, P, P, P, PLAN,
                                c_i64, P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P,
                                P, P, P, P, P, P, P, c_sz, P]),
+    "gfd_gat_bwd_mode": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P, PLAN, P, P, P, PLAN,
+                                 c_i64, P, P, P, ct.c_int, ct.c_int, c_f32, c_f32, c_u64, P, P, P,
+                                 P, P, P, P, P, P, ct.c_int, P, c_sz, P]),
     "gfd_x_colmax": (c_i32, [P, ct.c_int, c_i64, ct.c_int, c_i64, P, P]),
 }
 

@@ -905,15 +905,23 @@ def all_reduce_grads(params, group=None) -> None:
     """Sum the ranks' partial parameter gradients (one flat all-reduce; the
     reference layer's W, att_src, att_dst, bias: 0.35 MB at F = 166)."""
     import torch.distributed as dist
-    ps = [p for p in params if p.grad is not None]
+    ps = [p for p in params if p.requires_grad]
     if not ps or dist.get_world_size(group) == 1:
         return
-    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    # every parameter in the same order on every rank, a missing gradient as
+    # zeros (a rank whose shard never touched a parameter, set_to_none=True):
+    # the flat buffers then line up element for element (ADVICE r5)
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
+                      for p in ps])
     dist.all_reduce(flat, group=group)
     off = 0
     for p in ps:
-        n = p.grad.numel()
-        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        n = p.numel()
+        g = flat[off:off + n].view_as(p)
+        if p.grad is None:
+            p.grad = g.clone()
+        else:
+            p.grad.copy_(g)
         off += n
 
 
@@ -1003,6 +1011,11 @@ class _ShardedBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, weight, bias, n_total, eps, group):
+        # affine=False: weight 1, bias 0 (and no gradients for them)
+        ctx.affine = weight is not None
+        if weight is None:
+            weight = torch.ones(y.size(1), dtype=y.dtype, device=y.device)
+            bias = torch.zeros(y.size(1), dtype=y.dtype, device=y.device)
         yd = y.double()
         sums = torch.cat([yd.sum(0), (yd * yd).sum(0)])
         _all_reduce(sums, group)
@@ -1027,6 +1040,8 @@ class _ShardedBN(torch.autograd.Function):
         _all_reduce(sums, ctx.group)
         C, n = g.size(1), ctx.n_total
         dy = (weight.double() * invstd.double() / n) * (n * gd - sums[:C] - xd * sums[C:])
+        if not ctx.affine:
+            return dy.to(g.dtype), None, None, None, None, None
         return dy.to(g.dtype), grad_weight_part, grad_bias_part, None, None, None
 
 

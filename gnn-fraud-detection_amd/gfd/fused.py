@@ -64,6 +64,25 @@ def head_foldable(head, width: int, conv=None) -> bool:
             (head.bias is None or head.bias.dtype == torch.float32))
 
 
+def check_params(conv, bn, device) -> None:
+    """The checks GATConvFunction.forward makes on the layer's tensors, for the
+    packed-weights inference paths (eval_conv, gat_layer): their pointers go
+    to the kernels on x's stream, so a parameter left on the CPU, on another
+    GPU or in another dtype must raise here, not fault or read garbage there
+    (ADVICE r5)."""
+    from .nn import _check_tensor
+    _check_tensor("lin_src.weight", conv.lin_src.weight, device)
+    _check_tensor("att_src", conv.att_src, device)
+    _check_tensor("att_dst", conv.att_dst, device)
+    if conv.bias is not None:
+        _check_tensor("bias", conv.bias, device)
+    if bn is not None:
+        for n in ("running_mean", "running_var", "weight", "bias"):
+            t = getattr(bn, n, None)
+            if t is not None:
+                _check_tensor(f"BatchNorm {n}", t, device)
+
+
 def eval_weights(conv, bn, device) -> Tuple[torch.Tensor, torch.Tensor]:
     """(packed weights, BatchNorm scale | shift) of an inference layer, rebuilt
     only when a tensor they derive from changed: the cache on ``conv`` holds
@@ -112,6 +131,7 @@ def eval_conv(conv, x: torch.Tensor, edge_index) -> torch.Tensor:
     N, F = x.shape
     if F != conv.lin_src.weight.size(1):
         raise ValueError(f"x has {F} features, the layer expects {conv.lin_src.weight.size(1)}")
+    check_params(conv, None, dev)
     packed, _ = eval_weights(conv, None, dev)
     bias = conv.bias.detach() if conv.bias is not None else None
     plan = graph.plan()
@@ -138,6 +158,7 @@ def gat_layer(conv, bn, h: torch.Tensor, edge_index, relu: bool = True,
     x = _rows(h)
     N, F = x.shape
     bias = conv.bias.detach() if conv.bias is not None else None
+    check_params(conv, bn, dev)
     packed, ab = eval_weights(conv, bn, dev)
     res = None
     if residual:

@@ -356,13 +356,13 @@ def _poll_pending(block: bool = False) -> None:
     bad = None
     done = []
     for item in pend:
-        ev, flag, akey, what = item
+        ev, flag, akey, what, oid, ref = item
         if not block and not ev.query():
             continue
         ev.synchronize()        # complete already (or block): returns at once
         done.append(item)
         if int(flag[0]) != 0 and bad is None:
-            bad = (akey, what)
+            bad = (akey, what, oid, ref)
     if done:
         with _LOCK:
             for item in done:
@@ -370,6 +370,11 @@ def _poll_pending(block: bool = False) -> None:
                     _PENDING.remove(item)
             if bad is not None:
                 _BY_ADDR.pop(bad[0], None)
+                # and the object entry the speculated hit created: the next
+                # lookup of that same tensor must re-fingerprint it
+                ent = _BY_ID.get(bad[2])
+                if ent is not None and ent[0]() is not None and ent[0]() is bad[3]():
+                    _BY_ID.pop(bad[2], None)
     if bad is not None:
         raise GraphChangedError(
             f"gfd: an edge_index {bad[1]} was allocated where a cached graph's edge list had "
@@ -401,7 +406,8 @@ def _speculate(edge_index: torch.Tensor, akey, g: "CSRGraph", fp_cached: torch.T
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(edge_index.device))
     with _LOCK:
-        _PENDING.append((ev, host, akey, f"of shape {tuple(edge_index.shape)}"))
+        _PENDING.append((ev, host, akey, f"of shape {tuple(edge_index.shape)}",
+                         id(edge_index), weakref.ref(edge_index)))
 
 
 def get_graph(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:

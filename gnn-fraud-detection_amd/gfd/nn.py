@@ -15,6 +15,7 @@ Forward and backward both run in libgfd.so (``gfd_gat_fwd`` /
 from __future__ import annotations
 
 import math
+import os
 import weakref
 from collections import OrderedDict
 from typing import Optional
@@ -107,17 +108,26 @@ class GATConvFunction(torch.autograd.Function):
         ws = _ws(lib.gfd_gat_bwd_workspace_size(N, graph.num_messages, F, H, C, plan.num_hubs,
                                                 plan.num_chunks, splan.num_chunks), dev)
         cm = x_colmax(x)
-        _lib.call("gfd_gat_bwd_ex", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
+        _lib.call("gfd_gat_bwd_mode", x.data_ptr(), _lib.x_dtype_code(x), N, F, x.stride(0),
                   graph.rowptr.data_ptr(), graph.col.data_ptr(), plan.cstruct(),
                   csc.colptr.data_ptr(), csc.dst.data_ptr(), csc.eid.data_ptr(), splan.cstruct(),
                   graph.num_messages, weight.data_ptr(), att_src.data_ptr(),
                   att_dst.data_ptr(), H, C, slope, dp, seed & (2 ** 64 - 1), st.data_ptr(),
                   stats.data_ptr(), g.data_ptr(), _lib.ptr(gx), gw.data_ptr(), gas.data_ptr(),
-                  gad.data_ptr(), _lib.ptr(gb), cm.data_ptr(), ws.data_ptr(), ws.numel(),
-                  _lib.stream_handle(dev))
+                  gad.data_ptr(), _lib.ptr(gb), cm.data_ptr(), bwd_mode(), ws.data_ptr(),
+                  ws.numel(), _lib.stream_handle(dev))
         if gx is not None and x.dtype != torch.float32:
             gx = gx.to(x.dtype)
         return gx, gw, gas, gad, gb, None, None, None, None, None
+
+
+def bwd_mode() -> int:
+    """The backward dataflow gfd_gat_bwd_mode is asked for: GFD_BWD_DH (0, the
+    default) or, opt-in for A/B runs and tests, the fused source pass
+    (environment GFD_BWD_FUSED=1: 8-wave blocks, =2: 16-wave).  Read here, per
+    call, and passed explicitly: the C library itself reads no environment."""
+    v = os.environ.get("GFD_BWD_FUSED", "0")
+    return {"1": 1, "2": 2}.get(v, 0)
 
 
 # Per-column maxima of |x| -- the scales of the backward's grad_W GEMM -- kept

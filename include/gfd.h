@@ -508,6 +508,28 @@ gfd_status gfd_gat_bwd_ex(const void* x, int x_dtype, int64_t num_nodes, int in_
                           float* grad_bias, const uint32_t* x_colmax, void* ws, size_t ws_bytes,
                           gfd_stream_t stream);
 
+/* gfd_gat_bwd_ex with the backward's dataflow chosen by the caller (ABI 7;
+ * the library reads no environment):
+ *   GFD_BWD_DH       the source pass writes dh' rows, the grad_W' GEMM reads
+ *                    them (the default of gfd_gat_bwd / gfd_gat_bwd_ex);
+ *   GFD_BWD_FUSED8   the fused source pass + grad_W' GEMM (k_src_gw), 8-wave
+ *   GFD_BWD_FUSED16  or 16-wave blocks, taken only when grad_x is NULL and
+ *                    in_features <= 192 (otherwise the dh' path runs).
+ * Any other mode: GFD_ERR_ARGUMENT.  Replaces the same reference interface as
+ * gfd_gat_bwd (loss.backward(), train.py:142). */
+enum { GFD_BWD_DH = 0, GFD_BWD_FUSED8 = 1, GFD_BWD_FUSED16 = 2 };
+gfd_status gfd_gat_bwd_mode(const void* x, int x_dtype, int64_t num_nodes, int in_features,
+                            int64_t x_stride, const int32_t* rowptr, const int32_t* col,
+                            const gfd_plan* plan, const int32_t* colptr, const int32_t* csc_dst,
+                            const int32_t* csc_eid, const gfd_plan* src_plan,
+                            int64_t num_messages, const float* weight, const float* att_src,
+                            const float* att_dst, int heads, int channels, float negative_slope,
+                            float dropout_p, uint64_t dropout_seed, const float* st,
+                            const float* stats, const float* grad_out, float* grad_x,
+                            float* grad_weight, float* grad_att_src, float* grad_att_dst,
+                            float* grad_bias, const uint32_t* x_colmax, int mode, void* ws,
+                            size_t ws_bytes, gfd_stream_t stream);
+
 /* Per-column maxima of |x| over rows [0, num_nodes) as float bits into
  * colmax (uint32 [in_features], in_features <= 256), for gfd_gat_bwd_ex. */
 gfd_status gfd_x_colmax(const void* x, int x_dtype, int64_t num_nodes, int in_features,

@@ -227,3 +227,65 @@ def test_sharded_model_train_step_matches_single_process(world, balance):
         want = model.out(h)
     assert_close_scaled(torch.from_numpy(eval_logits), want, rtol=1e-10,
                         what=f"sharded eval logits, world {world}")
+
+
+# ---------------------------------------------------------------------------
+# all_reduce_grads with ranks that disagree about which gradients
+# exist, and sharded_batch_norm without an affine transform.
+
+def _advice_rank(rank, world, path, q):
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
+    try:
+        # rank 1 never touched the second parameter (its grad is None there)
+        ps = [torch.zeros(3, requires_grad=True), torch.zeros(2, requires_grad=True),
+              torch.zeros(4, requires_grad=True)]
+        ps[0].grad = torch.full((3,), float(rank + 1))
+        if rank == 0:
+            ps[1].grad = torch.tensor([5.0, 7.0])
+        ps[2].grad = torch.arange(4.0) * (rank + 1)
+        gdist.all_reduce_grads(ps)
+        # BatchNorm1d(affine=False) on this rank's rows of a 2-rank batch
+        gen = torch.Generator().manual_seed(3)
+        y_all = torch.randn(10, 4, generator=gen, dtype=torch.float64)
+        rows = y_all[:6] if rank == 0 else y_all[6:]
+        y = rows.clone().requires_grad_(True)
+        bn = torch.nn.BatchNorm1d(4, affine=False).double()
+        out = gdist.sharded_batch_norm(y, bn, 10)
+        g_all = torch.randn(10, 4, generator=gen, dtype=torch.float64)
+        (out * (g_all[:6] if rank == 0 else g_all[6:])).sum().backward()
+        q.put((rank, [p.grad.clone() for p in ps], out.detach(), y.grad.clone(),
+               bn.running_mean.clone(), bn.running_var.clone()))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_all_reduce_grads_missing_grads_and_bn_without_affine():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = _store_path()
+    procs = [ctx.Process(target=_advice_rank, args=(r, 2, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=180), q.get(timeout=180)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        grads = res[rank][0]
+        assert torch.equal(grads[0], torch.full((3,), 3.0))
+        assert torch.equal(grads[1], torch.tensor([5.0, 7.0]))   # rank 1's None counted as 0
+        assert torch.equal(grads[2], torch.arange(4.0) * 3)
+    gen = torch.Generator().manual_seed(3)
+    y_all = torch.randn(10, 4, generator=gen, dtype=torch.float64).requires_grad_(True)
+    bn = torch.nn.BatchNorm1d(4, affine=False).double()
+    ref_out = bn(y_all)
+    g_all = torch.randn(10, 4, generator=gen, dtype=torch.float64)
+    (ref_out * g_all).sum().backward()
+    out = torch.cat([res[0][1], res[1][1]])
+    gy = torch.cat([res[0][2], res[1][2]])
+    assert torch.allclose(out, ref_out.detach(), atol=1e-12)
+    assert torch.allclose(gy, y_all.grad, atol=1e-12)
+    for rank in (0, 1):
+        assert torch.allclose(res[rank][3], bn.running_mean, atol=1e-12)
+        assert torch.allclose(res[rank][4], bn.running_var, atol=1e-12)

@@ -62,3 +62,24 @@ def test_fused_layers_rebuild_on_new_batchnorm_statistics():
     m2.load_state_dict(m.state_dict())
     with torch.no_grad():
         assert torch.equal(m2(x, graph), c)                     # fresh caches agree
+
+
+def test_module_parameters_on_the_wrong_device_or_dtype_raise():
+    """the packed-weights inference path checks the layer's own
+    tensors (device, dtype) before their pointers reach a kernel."""
+    from gfd import graph as gg
+    from gfd.nn import GATConv
+    x_cpu, ei, _ = _random_case(600, 3000, 166, seed=3, kind="powerlaw")
+    x = x_cpu.to(DEV)
+    graph = gg.get_graph(ei.to(DEV), 600)
+    conv = GATConv(166, 64, heads=8, concat=False).eval()        # left on the CPU
+    with torch.no_grad():
+        with pytest.raises(RuntimeError, match="HIP device"):
+            conv(x, graph)
+        conv = conv.to(DEV).double()                               # wrong dtype
+        with pytest.raises(TypeError, match="float32"):
+            conv(x, graph)
+        conv = conv.float()
+        conv.bias.data = conv.bias.data.cpu()                     # one tensor left behind
+        with pytest.raises(RuntimeError, match="bias"):
+            conv(x, graph)

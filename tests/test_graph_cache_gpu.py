@@ -66,6 +66,11 @@ def test_changed_edges_at_a_reused_address_raise():
     torch.cuda.synchronize()
     with pytest.raises(gg.GraphChangedError):
         gg.sync_pending_checks()            # ... and caught by the device-side check
+    # the object entry the speculated hit made is gone too: the
+    # same tensor, looked up again, is fingerprinted and gets its own graph
+    gb = gg.get_graph(b, 3000)
+    assert gb is not g1
+    assert torch.equal(gb.col, gg.csr_from_coo(b, 3000).col)
     # the address entry is gone: the next lookup takes the fingerprint path
     c = b.clone()
     del b
