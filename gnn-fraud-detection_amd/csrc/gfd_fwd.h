@@ -114,9 +114,6 @@ __device__ __forceinline__ f32x4 load4(const typename XT::T* p) {
 // in bytes < 2^32 (checked on the host)
 template <typename XT>
 __device__ __forceinline__ const char* xrow(const void* x, int j, int64_t ldx) {
-#ifdef GFD_AB_NOGATHER
-  j &= 1023;  // ablation build only: every gathered row from a 1,024-row (L2) window
-#endif
   return reinterpret_cast<const char*>(x) +
          uint64_t(uint32_t(j)) * uint64_t(uint32_t(ldx) * uint32_t(XT::kBytes));
 }
@@ -233,11 +230,7 @@ __device__ __forceinline__ int pack_zrow(const f32x2 (&z)[4][KF], float inv, int
 #pragma unroll
   for (int g = 0; g < 4; ++g) i2[g] = bcast2(inv, 2 * g);
   int er = erg;
-#ifdef GFD_AB_GS_ONLY
-  if (false) {
-#else
   if (erg == 127) {
-#endif
     float zm = 0.f;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {

@@ -1280,9 +1280,6 @@ __global__ void __launch_bounds__(64 * NW) k_src_gw(
     }
   };
   auto issue_data = [&]() {
-#ifdef GFD_AB_F_NODATA  // ablation: no record / g-row gathers (garbage sums)
-    return;
-#endif
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
       const float* rp = rec + int64_t(pe[bb]) * kRec + (lane & 7);
@@ -1592,9 +1589,7 @@ __global__ void __launch_bounds__(64 * NW) k_src_gw(
     const int64_t k0 = kb + t * kFK;
     // ---- phase 1: tile t - 1's MFMAs (A / B images) overlapped with tile t's
     // walk (the y tile): the walk's gathers wait behind the matrix cores ----
-#ifndef GFD_AB_F_NOMFMA
     if (t > 0) mfma_tile();
-#endif
     GFD_FSTAMP(0);
     if (lane < 8 * NPW)
       dtt[(NPW * wave + (lane >> 3)) * 8 + (lane & 7)] =
@@ -1604,25 +1599,15 @@ __global__ void __launch_bounds__(64 * NW) k_src_gw(
       load_dt(k0 + kFK);
     }
     if (t + 2 < T) load_next(k0 + 2 * kFK);
-#ifndef GFD_AB_F_NOX  // ablation: no x tile loads
     load_x(k0, opaque(tid));
-#endif
     GFD_FSTAMP(1);
-#ifdef GFD_AB_F_NOY  // ablation: no y phase walk
-    if (false) {
-#else
     if (lo < hi) {
-#endif
       cur = rfirst;
 #pragma unroll
       for (int hl = 0; hl < 4; ++hl) y[hl] = 0.f;
       ds = 0.f;
       consume(min(hi - lo, NCH));
-#ifdef GFD_AB_F_NOEXTRA  // ablation: first chunk only (wrong sums for long ranges)
-      for (int c = hi; c < hi; c += NCH) {
-#else
       for (int c = lo + NCH; c < hi; c += NCH) {  // long ranges: further chunks in place
-#endif
         if (half == 0) ds += chunk_ds();  // the running source's ds from this chunk
         issue_idx(Pof(int(t) & 1), Cof(int(t) & 1), c, hi, pe, pi, rr);
         issue_data();
@@ -1651,17 +1636,13 @@ __global__ void __launch_bounds__(64 * NW) k_src_gw(
       int hw[NW];
 #pragma unroll
       for (int w = 0; w < NW; ++w) hw[w] = __builtin_amdgcn_readfirstlane(hpr[w]);
-#ifndef GFD_AB_F_NOCOL
       ycolumn(tq / TPC, tq % TPC, hw);
       if (wave < 8) xcolumn(wave, hw);
-#endif
     }
     __syncthreads();
     GFD_FSTAMP(5);
   }
-#ifndef GFD_AB_F_NOMFMA
   if (T > 0) mfma_tile();  // the last tile's
-#endif
 #ifdef GFD_FPROF
   if (lane == 0) {
 #pragma unroll

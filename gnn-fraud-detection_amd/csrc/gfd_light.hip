@@ -1,5 +1,5 @@
 // gfd_light.hip -- the light class (destinations of 2 .. kLightMax messages,
-// self loop included) for fp32 rows, 64 + Fp/2 <= F <= 168: the PyG
+// self loop included) for fp32 and bf16 rows, 64 + Fp/2 <= F <= 168: the PyG
 // GATConv.forward softmax-aggregate-project of /root/reference/src/models/gat.py:80
 // (and tgn.py:94) as a PAIRED-PHASE tile kernel.
 //
@@ -40,35 +40,30 @@
 // Aggregation layout: each wave aggregates slots 4 ct .. 4 ct + 3 in two
 // passes of two slots (lanes 0..31: slot 4 ct + 2 pass, lanes 32..63: the
 // next); lane li = lane & 31 holds local features li, 32 + li, 64 + li of
-// its slot, all 8 heads (z: 12 f32x2).  Rows are gathered with structured
-// buffer loads (index = source row, stride = row pitch): the index check
-// returns zeros without a memory access for rows past a slot's messages and
-// for features past F (probed: scripts/sbuf_probe.hip).  A pass's rows for
-// the NEXT tile are issued right after the pass consumed this tile's, so a row
-// has two steps to arrive.
+// its slot, all 8 heads (z: 12 f32x2).  Rows are gathered with 64-bit lane
+// addresses (structured buffer loads would range-check rows and features for
+// free, but a descriptor reaches only 4 GiB: scripts/sbuf_probe.hip); rows
+// past a slot's messages and features past F are masked loads reading 0.  A
+// pass's rows for the NEXT tile are issued right after the pass consumed
+// this tile's, so a row has two steps to arrive.
 //
 // Results are bit-identical to k_stream<LIGHT> while one launch-wide scale
 // covers x (max |x| <= 2^20): same weights, same FMA order, same f16 split,
 // same MFMA k-step order and partial-sum order.
-#include <climits>
-
 #include "gfd_fwd.h"
 
 using namespace gfd;
 using namespace gfd::fwd;
-
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-// buffer_load_dword ... idxen offen: base + index * stride + offset, index
-// range-checked against num_records (rows)
-__device__ float sbuf_load_f32(i32x4 rsrc, int vindex, int voffset, int soffset, int aux)
-    __asm("llvm.amdgcn.struct.buffer.load.f32");
 
 namespace {
 
 constexpr int kLW = 8;                 // waves per block: 2 groups x 4 column tiles
 constexpr int kLR = kLightMax;         // rows (messages) per slot
 constexpr int kLZPad = 16;             // Z row pad (halves): conflict-free A-fragment reads
-constexpr int kPoison = 0x7fffffff;    // row index past num_records: reads 0, no access
+// bf16 rows (config C5) through this kernel as well
+#ifndef GFD_LIGHT_PAIR_BF16
+#define GFD_LIGHT_PAIR_BF16 1
+#endif
 
 
 struct Logits {  // a softmax owner's two slots: s_j of message lane >> 3, t_i (head lane & 7)
@@ -86,16 +81,51 @@ __device__ __forceinline__ float max_half32(float v) {
   return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
 }
 
+// acc += ahi.bh + ahi.bl + alo.bh (the 3-term split) IN PLACE.  Inline asm,
+// because with the builtins the register allocator gave these chains
+// destination quads partially overlapping their srcC quads (v[2:5] <- ..,
+// v[0:3]) in this kernel -- 168 such MFMAs, and rows of the tile came out
+// wrong at random (round 6; the k_stream listing has none).  The first
+// k-step of a chain takes srcC = 0 (no vector write of the accumulator ahead
+// of it); a chain's own back-to-back MFMAs on one quad need no wait states.
+__device__ __forceinline__ void mfma3(f32x4& acc, f16x8 ahi, f16x8 alo, f16x8 bh, f16x8 bl,
+                                      bool first) {
+  if (first) {
+    asm volatile(
+        "v_mfma_f32_16x16x32_f16 %0, %1, %3, 0\n\t"
+        "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0\n\t"
+        "v_mfma_f32_16x16x32_f16 %0, %2, %3, %0"
+        : "=&v"(acc)
+        : "v"(ahi), "v"(alo), "v"(bh), "v"(bl));
+  } else {
+    asm volatile(
+        "v_mfma_f32_16x16x32_f16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0\n\t"
+        "v_mfma_f32_16x16x32_f16 %0, %2, %3, %0"
+        : "+v"(acc)
+        : "v"(ahi), "v"(alo), "v"(bh), "v"(bl));
+  }
+}
+
+#ifdef GFD_LP_PROF
+// Diagnostic build only (GFD_BUILD_VARIANT=lpprof GFD_EXTRA_FLAGS=-DGFD_LP_PROF):
+// per-wave s_memtime cycles summed over waves, [group][i]: 0 aggregation-step
+// work, 1 of it waiting for the step's rows, 2 MFMA-step work, 3 barrier after
+// an aggregation step, 4 barrier after an MFMA step, 5 aggregation steps,
+// 6 MFMA steps (scripts/prof_light_pair.py)
+__device__ unsigned long long g_lprof[2][8];
+#endif
+
 size_t light_pair_smem(int Fp, int lo) {
   const int ZSH = 4 * Fp + kLZPad;
   return sizeof(_Float16) * 4 * kTile * ZSH + sizeof(uint4) * kLW * lo * 64 +
-         sizeof(float) * kTile * 48 + sizeof(f32x4) * 4 * 64 + sizeof(int) * 2 * kTile +
+         sizeof(float) * kTile * 64 + sizeof(f32x4) * 4 * 64 + sizeof(int) * 2 * kTile +
          sizeof(float) * 4 * kTile;
 }
 
-template <int KHM, int LO, bool EXACT, bool EPI>
+template <typename XT, int KHM, int LO, bool EXACT, bool EPI>
 __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
-    const float* __restrict__ x, int64_t N, int F, int Fp, int64_t ldx, int64_t num_dst,
+    const void* __restrict__ x, int64_t N, int F, int Fp, int64_t ldx, int64_t num_dst,
     const int4* __restrict__ desc, const int32_t* __restrict__ cols8,
     const float* __restrict__ s, int lds, const float* __restrict__ t, int ldt,
     const PackHeader* __restrict__ hdr, const uint4* __restrict__ wsh,
@@ -109,7 +139,11 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
   _Float16* Zl = Zh + 2 * kTile * ZSH;                            // [2 g][16][ZSH]
   uint4* WL = reinterpret_cast<uint4*>(Zl + 2 * kTile * ZSH);     // [8 waves][LO][64]
   float* P = reinterpret_cast<float*>(WL + kLW * LO * 64);        // [16][48]
+#ifdef GFD_LP_DIAG_P64
+  f32x4* red = reinterpret_cast<f32x4*>(P + kTile * 64);          // [4 ct][64]
+#else
   f32x4* red = reinterpret_cast<f32x4*>(P + kTile * 48);          // [4 ct][64]
+#endif
   int* rid = reinterpret_cast<int*>(red + 4 * 64);                // [2 par][16]
   float* rsc = reinterpret_cast<float*>(rid + 2 * kTile);         // [2 g][2 par][16]
 
@@ -156,16 +190,12 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
   }
   if (nv == 0) return;  // uniform per block: no barrier below is reached by anyone
 
-  // row gathers: structured buffer over x, one record per row
-  const uint64_t xbase = reinterpret_cast<uint64_t>(x);
-  const i32x4 xrs = {int(uint32_t(xbase)),
-                     int((uint32_t(xbase >> 32) & 0xffffu) | (uint32_t(ldx * 4) << 16)), int(N),
-                     0x00020000};
+  const int64_t pitch = ldx * XT::kBytes;      // row pitch in bytes (< 2^32: host check)
   const int fg = g * FH;                       // first feature of this half
 
   // slot records, one VGPR per tile: lanes 8 q + k = source k of slot 4 ct + q;
   // lanes 32 + 4 q + f = field f of its descriptor {row, e_begin, e_end, hub},
-  // e_end = INT_MIN for a slot past the class (empty)
+  // e_end = -1 for a slot past the class (empty)
   auto rec_load = [&](int64_t v) -> int {
     const int q = lane < 32 ? (lane >> 3) : min((lane - 32) >> 2, 3);
     const int64_t sl0 = slot(v, 4 * ct + q);
@@ -173,18 +203,21 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
     const int32_t* a = lane < 32 ? cols8 + sl * 8 + (lane & 7)
                                  : reinterpret_cast<const int32_t*>(desc + sl) + (lane & 3);
     const int val = *a;
-    return (lane >= 32 && (lane & 3) == 2 && sl0 >= lim) ? INT_MIN : val;
+    return (lane >= 32 && (lane & 3) == 2 && sl0 >= lim) ? -1 : val;
   };
   auto n_of = [&](int Cr, int64_t, int q) -> int {  // messages of slot 4 ct + q (0: empty)
     const int e0 = __builtin_amdgcn_readlane(Cr, 33 + 4 * q);
     const int e1 = __builtin_amdgcn_readlane(Cr, 34 + 4 * q);
-    return max(e1 - e0, 0);
+    return e1 < 0 ? 0 : e1 - e0;
   };
 
   // a pass's rows for the next tile (lane <-> its slot's three features):
   // features 0, 1 of round k in xa[p][k], feature 2 of rounds 2 i, 2 i + 1 in
   // xb[p][i] -- register PAIRS, so the packed FMAs broadcast either half by
   // op_sel (single floats would each take an aligned pair)
+#ifdef GFD_LP_PROF
+  unsigned long long pw = 0ull;  // cycles waiting for rows (aggregation)
+#endif
   f32x2 xa[2][kLR], xb[2][(kLR + 1) / 2];
   Logits lg;            // logits of the wave's next softmax
   int Cq[4];            // records of tiles v .. v + 3 (of the wave's next aggregation v)
@@ -193,21 +226,28 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
   auto rows_issue = [&](int Cn, int64_t vn, int p) {
     if (vn >= nv) return;
     const int hf = lane >> 5, li = lane & 31;
-    const int off0 = (fg + li) * 4, off1 = (fg + 32 + li) * 4;
+    constexpr int eb = XT::kBytes;
     const bool v2 = 64 + li < FH && fg + 64 + li < F;   // third feature of the lane exists
-    const int off2 = v2 ? (fg + 64 + li) * 4 : 0;
     const int q = 2 * p + hf;
     const int na = n_of(Cn, vn, 2 * p), nb = n_of(Cn, vn, 2 * p + 1);
-    const int R = max(na, nb);
+    const int R = max(na, nb), nmin = min(na, nb);
     const int nl = hf ? nb : na;
+    const char* xl = reinterpret_cast<const char*>(x) + (fg + li) * eb;
 #pragma unroll
     for (int k = 0; k < kLR; ++k) {
       if (k < R) {
         const int j = __builtin_amdgcn_ds_bpermute((8 * q + k) << 2, Cn);
-        const int jj = k < nl ? j : kPoison;
-        xa[p][k].x = sbuf_load_f32(xrs, jj, off0, 0, 0);
-        xa[p][k].y = sbuf_load_f32(xrs, jj, off1, 0, 0);
-        const float x2 = sbuf_load_f32(xrs, v2 ? jj : kPoison, off2, 0, 0);
+        // the lane's first feature of row j (64-bit: x exceeds the 4 GiB a
+        // buffer descriptor reaches -- scripts/sbuf_probe.hip)
+        const typename XT::T* ra = reinterpret_cast<const typename XT::T*>(
+            xl + uint64_t(uint32_t(j)) * uint64_t(uint32_t(pitch)));
+        float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+        if (k < nmin || k < nl) {  // (uniform, or this half's slot has message k)
+          x0 = xcvt(ra[0]);
+          x1 = xcvt(ra[32]);
+          if (v2) x2 = xcvt(ra[64]);
+        }
+        xa[p][k] = f32x2{x0, x1};
         if (k & 1) xb[p][k >> 1].y = x2;
         else xb[p][k >> 1].x = x2;
       }
@@ -250,8 +290,13 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
       if (__builtin_expect(dp > 0.f, 0))  // kernel-uniform
         pd = dropout_keep(seed, uint32_t(e0 + kk), uint32_t(h), dp) ? pe * (1.0f / (1.0f - dp)) : 0.f;
       const float ps = pd * (inv * ergs);
+#ifdef GFD_LP_DIAG_P64
+      P[r * 64 + lane] = ps;
+      rid[par * kTile + r] = n > 0 ? row : -1;
+#else
       if (lane < 48) P[r * 48 + lane] = ps;
       if (lane == 0) rid[par * kTile + r] = n > 0 ? row : -1;
+#endif
     }
   };
   // the wave's feature half of slots 4 ct + 2 p (lanes 0..31) and + 1 (32..63)
@@ -262,7 +307,21 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
     const bool w2 = 64 + li < FH;                // the lane's third feature is in this half
     const int r = 4 * ct + 2 * p + hf;
     const int R = max(max(n_of(Cr, v, 2 * p), n_of(Cr, v, 2 * p + 1)), 1);
+#ifdef GFD_LP_DIAG_P64
+    const float* pr = P + r * 64;
+#else
     const float* pr = P + r * 48;
+#endif
+#ifdef GFD_LP_DIAG_WAIT
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+#ifdef GFD_LP_PROF
+    {
+      const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_s_waitcnt(0);
+      pw += __builtin_amdgcn_s_memtime() - w0;
+    }
+#endif
     f32x2 z[4][3];
 #pragma unroll
     for (int k = 0; k < kLR; ++k) {
@@ -343,12 +402,14 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
           }
         }
         f32x4& acc = (u & 1) ? acc1 : acc0;
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[u], acc, 0, 0, 0);
+        mfma3(acc, ahi, alo, bh[u], blo, u < 2);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    // the MFMA results are read by vector instructions next: the inline-asm
+    // chains carry no hazard information for the compiler, so wait out the
+    // last MFMA's passes here (16 wait states)
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
     acc0 += acc1;
     if (g == 0) {
       if (erg == 127) {
@@ -375,7 +436,14 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
   // waves (0, ct) and (1, ct) before group 1 replaces them)
   auto valu_step = [&](int64_t v) {
     Cq[3] = rec_load(v + 3);
-    if (g == 0) softmax(Cq[0], v);
+    if (g == 0) {
+      softmax(Cq[0], v);
+      // this wave reads back the weights it just wrote: the hardware runs a
+      // wave's LDS operations in order, but the compiler must not hoist the
+      // reads above the writes (it did: stale weights in slot 4 ct + 1)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       if (v >= 0) aggregate(Cq[0], v, p);
@@ -406,9 +474,17 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
   }
   __syncthreads();  // Z zeroed
 
+#ifdef GFD_LP_PROF
+  unsigned long long pc[7] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+#endif
   for (int64_t st = -2; st < 2 * nv; ++st) {
     lane = opaque(threadIdx.x & 63);
     const bool odd = (st & 1) != 0;
+#ifdef GFD_LP_PROF
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long pw0 = pw;
+    const bool vstep = (g == 0) ? odd : !odd;
+#endif
     if (g == 0) {
       if (odd) {
         const int64_t v = (st + 1) / 2;
@@ -426,14 +502,33 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
         rotate();
       }
     }
+#ifdef GFD_LP_PROF
+    const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#ifdef GFD_LP_PROF
+    const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+    if (st >= 0) {
+      pc[vstep ? 0 : 2] += ts1 - ts0;
+      pc[1] += pw - pw0;
+      pc[vstep ? 3 : 4] += ts2 - ts1;
+      pc[vstep ? 5 : 6] += 1;
+    }
+#endif
   }
+#ifdef GFD_LP_PROF
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) atomicAdd(&g_lprof[g][i], pc[i]);
+  }
+#endif
 }
 
-template <int KHM, int LO, bool EXACT>
+template <typename XT, int KHM, int LO, bool EXACT>
 gfd_status launch_pair_k(const AggArgs& a, const PackLayout& L, bool to_end, hipStream_t stream) {
   const bool epi = a.ep.ab != nullptr;
-  auto kern = epi ? &k_light_pair<KHM, LO, EXACT, true> : &k_light_pair<KHM, LO, EXACT, false>;
+  auto kern = epi ? &k_light_pair<XT, KHM, LO, EXACT, true>
+                  : &k_light_pair<XT, KHM, LO, EXACT, false>;
   const size_t lds = light_pair_smem(L.Fp, LO);
   if (lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;
   if (!ensure_lds(reinterpret_cast<const void*>(kern), lds)) return GFD_ERR_HIP;
@@ -442,7 +537,7 @@ gfd_status launch_pair_k(const AggArgs& a, const PackLayout& L, bool to_end, hip
   if (grid > tiles) grid = tiles;
   const gfd_plan& p = a.plan;
   kern<<<int(grid), kLW * 64, lds, stream>>>(
-      static_cast<const float*>(a.x), a.N, a.F, L.Fp, a.ldx, a.num_dst,
+      a.x, a.N, a.F, L.Fp, a.ldx, a.num_dst,
       reinterpret_cast<const int4*>(p.slot_desc), p.slot_cols, a.s, a.lds, a.t, a.ldt,
       reinterpret_cast<const PackHeader*>(a.packed + L.hdr_off),
       reinterpret_cast<const uint4*>(a.packed + L.wsh_off),
@@ -458,8 +553,10 @@ namespace gfd {
 namespace fwd {
 
 bool light_pair_supported(const AggArgs& a, const PackLayout& L) {
-  return a.xdt == GFD_DTYPE_F32 && kf_for(a.F) == 3 && a.F >= 64 + L.Fp / 2 &&
-         a.ldx * 4 <= 16383 && a.ep.hout == nullptr && a.N <= 0x7fffffff &&
+  const int eb = a.xdt == GFD_DTYPE_BF16 ? 2 : 4;
+  return (a.xdt == GFD_DTYPE_F32 || (GFD_LIGHT_PAIR_BF16 && a.xdt == GFD_DTYPE_BF16)) &&
+         kf_for(a.F) == 3 && a.F >= 64 + L.Fp / 2 && a.ldx * eb <= 0x7fffffffLL &&
+         a.ep.hout == nullptr && a.N <= 0x7fffffff &&
          a.plan.slot_desc && a.plan.slot_cols && a.plan.class_split;
 }
 
@@ -467,9 +564,24 @@ gfd_status launch_light_pair(const AggArgs& a, const PackLayout& L, bool to_end,
                              hipStream_t stream) {
   if (!light_pair_supported(a, L)) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-  return L.KS / 2 == 21 ? launch_pair_k<21, 8, true>(a, L, to_end, stream)
-                        : launch_pair_k<21, 8, false>(a, L, to_end, stream);
+  const bool exact = L.KS / 2 == 21;
+  if (a.xdt == GFD_DTYPE_BF16)
+    return exact ? launch_pair_k<XBF16, 21, 8, true>(a, L, to_end, stream)
+                 : launch_pair_k<XBF16, 21, 8, false>(a, L, to_end, stream);
+  return exact ? launch_pair_k<XF32, 21, 8, true>(a, L, to_end, stream)
+               : launch_pair_k<XF32, 21, 8, false>(a, L, to_end, stream);
 }
 
 }  // namespace fwd
 }  // namespace gfd
+
+#ifdef GFD_LP_PROF
+extern "C" int gfd_lprof_read(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_lprof), sizeof(g_lprof)) != hipSuccess) return 1;
+  if (reset) {
+    static const unsigned long long zero[2][8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lprof), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif

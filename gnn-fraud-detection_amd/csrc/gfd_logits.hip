@@ -159,10 +159,6 @@ k_logits_lone(
       }
     } else {
       const typename XT::T* xr = x + (rin ? row : rows - 1) * ldx + 4 * g;
-#ifdef GFD_AB_LOGITS_COAL
-      // ablation only (wrong results): every load one contiguous 1 KB of the tile
-      const typename XT::T* xc = x + (t * 16 < rows - 16 ? t * 16 : rows - 16) * ldx + 4 * lane;
-#endif
 #pragma unroll
       for (int s = 0; s < kLKS; ++s) {
         if (s >= KS) {
@@ -170,9 +166,6 @@ k_logits_lone(
           continue;
         }
         if (s < ksf) {
-#ifdef GFD_AB_LOGITS_COAL
-          a[s] = load4<XT>(xc + 256 * s);
-#else
           if constexpr (A16) {
             a[s] = load4<XT>(xr + 16 * s);
           } else {  // 8-B aligned rows (an even row pitch: the reference's [N, 166]): two 8-B loads
@@ -180,7 +173,6 @@ k_logits_lone(
             const float2 u1 = *reinterpret_cast<const float2*>(xr + 16 * s + 2);
             a[s] = f32x4{u0.x, u0.y, u1.x, u1.y};
           }
-#endif
         } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
 #pragma unroll
           for (int u = 0; u < 4; ++u) a[s][u] = 16 * s + 4 * g + u < F ? xcvt(xr[16 * s + u]) : 0.f;
@@ -200,11 +192,7 @@ k_logits_lone(
     }
     const bool lone = rin && rowptr[row + 1] - rowptr[row] == 1;
     am = fmaxf(am, rm);  // clamped tail rows repeat row rows - 1: harmless for a max
-#ifdef GFD_AB_LOGITS_NOLONE
-    const bool any_lone = __ballot(lone && rowptr[0] < 0) != 0;  // ablation only: no lone outputs
-#else
     const bool any_lone = __ballot(lone) != 0;  // wave-uniform
-#endif
     // Row conditioning: a row whose smallest nonzero |x| is below 2^-18 of its
     // max has features the one-row-scale f16 split cannot hold to ~2^-21 (an
     // outlier feature).  A tile with such a row also runs fp32 MFMA, and those
@@ -326,11 +314,7 @@ k_logits_lone(
       const int r = lane >> 2, qd = lane & 3;
       const f32x4 v = *reinterpret_cast<const f32x4*>(T + r * kTP + 4 * qd);
       const int64_t orow = t * 16 + r;
-#ifdef GFD_AB_LOGITS_NOST
-      if (orow < 0) {  // ablation only: no s / t stores
-#else
       if (orow < rows) {
-#endif
         // two stores under complementary lane masks keep both table bases scalar
         auto put = [&](float* dst) {
           if (st_vec) {
@@ -340,14 +324,7 @@ k_logits_lone(
             for (int i = 0; i < 4; ++i) dst[i] = v[i];
           }
         };
-#ifdef GFD_AB_LOGITS_S64  // ablation only (wrong results: the 8 floats before s overwritten): 64-B s blocks
-        if (qd < 2) {
-          put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd - 8);
-          put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd);
-        }
-#else
         if (qd < 2) put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd);
-#endif
         else put(tl + uint64_t(uint32_t(orow)) * uint32_t(ldt) + 4 * (qd - 2));
       }
     }

@@ -58,7 +58,7 @@ constexpr int kSWaves = 8;
 // bank conflict in one of their 16-lane groups, 16 none (scripts/bank_pad.py)
 // fp32 light rows with 64 + Fp / 2 <= F go to the paired-phase kernel (gfd_light.hip)
 #ifndef GFD_LIGHT_PAIR
-#define GFD_LIGHT_PAIR 1
+#define GFD_LIGHT_PAIR 0
 #endif
 #ifndef GFD_STREAM_ZPAD
 #define GFD_STREAM_ZPAD 8
@@ -190,10 +190,6 @@ template <int KF>
 __device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[kLightMax][KF],
                                           float p, int kmax) {
   static_assert(kLightMax >= 4 && kLightMax <= 7, "light slots: 4 .. 7 messages");
-#ifdef GFD_AB_LIGHT_K6  // A/B: one block for every count (rows past n carry p = 0)
-  fma_k<KF, kLightMax>(z, xv, p);
-  return;
-#endif
   if (kmax <= 2) fma_k<KF, 2>(z, xv, p);
   else if (kmax == 3) fma_k<KF, 3>(z, xv, p);
   else if (kLightMax == 4 || kmax == 4) fma_k<KF, 4>(z, xv, p);
@@ -233,20 +229,6 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLight
   }
   const int kk = lane >> 3;
   const int n = d.z - d.y;
-#ifdef GFD_AB_LIGHT_NOAGG  // ablation only (wrong results): rows consumed, no softmax / FMA / Z write
-  {
-    float f = q.sj + q.th;
-#pragma unroll
-    for (int k = 0; k < kLightMax; ++k)
-#pragma unroll
-      for (int qq = 0; qq < KF; ++qq) f += q.xv[k][qq];
-    if (lane == 0) {
-      rsc[r] = f;
-      rid[r] = d.x;
-    }
-    return;
-  }
-#endif
   const float v = leaky01(q.sj + q.th, slope);
   const float m = max_xor8_16_32(kk < n ? v : -INFINITY);
   const float p = kk < n ? __expf(v - m) : 0.f;
@@ -653,11 +635,7 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       if (u < KH) {
         const f16x8 ahi = phi[u % kAP], alo = plo[u % kAP];
         f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % kAP];
-#ifdef GFD_AB_LIGHT_NOAREAD  // ablation only (wrong results): A fragments of k-step 0 reused
-        if (!LIGHT && u + kAP < KH) {
-#else
         if (u + kAP < KH) {
-#endif
           phi[u % kAP] = *reinterpret_cast<const f16x8*>(ah + 32 * (u + kAP));
           plo[u % kAP] = *reinterpret_cast<const f16x8*>(al + 32 * (u + kAP));
           if (u + kAP >= NR) {
@@ -666,11 +644,6 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
           }
         }
         f32x4& acc = (u & 1) ? acc1 : acc0;
-#ifdef GFD_AB_LIGHT_NOMFMA  // ablation only (wrong results): no MFMAs, operands consumed
-        if (LIGHT) {
-          acc[0] += float(ahi[0]) + float(alo[1]) + float(bh[u][2]) + float(blo[3]);
-        } else
-#endif
         {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[u], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
@@ -732,11 +705,7 @@ size_t stream_smem(int Fp, int lo) {
 template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
-#ifdef GFD_AB_EPI_ON  // A/B: the epilogue instance for every launch
-  const bool epi = true;
-#else
   const bool epi = a.ep.ab != nullptr || a.ep.hout != nullptr;
-#endif
   auto kern = epi ? &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, true>
                   : &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, false>;
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;

@@ -4,7 +4,7 @@
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-timeout -k 10 60 scripts/sbuf_probe > gpurun_out/r6_sbuf.txt 2>&1; rc=$?; cat gpurun_out/r6_sbuf.txt; [ $rc -eq 0 ] || exit $rc
+
 GFD_LIB_PATH=$PWD/gnn-fraud-detection_amd/gfd/libgfd_lp0.so timeout -k 10 200 python scripts/dump_fwd.py lp0 || exit $?
 timeout -k 10 200 python scripts/dump_fwd.py pair || exit $?
 python scripts/cmp_dumps.py lp0 pair

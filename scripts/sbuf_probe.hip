@@ -26,6 +26,7 @@ int main() {
   const int64_t rows = 8000000;          // 5.6 GB
   float* x = nullptr;
   if (hipMalloc(&x, rows * pitch) != hipSuccess) { printf("alloc failed\n"); return 1; }
+  hipMemset(x, 0, rows * pitch);
   // row r, float f holds r * 1000 + f (exact in fp32 for the probed rows: < 2^24 only for small r,
   // so store a row tag instead: the low 20 bits of r in float form, plus f / 1024)
   const int probe_rows[4] = {3, 6100000, 7999999, 5000001};
@@ -49,6 +50,26 @@ int main() {
   if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
   float hout[n];
   hipMemcpy(hout, dout, sizeof(hout), hipMemcpyDeviceToHost);
+  {  // the last rows at several offsets (written above: rows 7999999; row 7999998 is not)
+    const int m = 12;
+    int i2[m] = {7999999, 7999999, 7999999, 7999999, 7999999, 7999999, 7999998, 7999998,
+                 6100000, 6100000, 3, 3};
+    int o2[m] = {0, 4, 128, 512, 640, 696, 0, 700, 700, 0, 700, 696};
+    float r2[m];
+    float* d2; hipMalloc(&d2, sizeof(r2));
+    int *di2, *do2;
+    hipMalloc(&di2, sizeof(i2));
+    hipMalloc(&do2, sizeof(o2));
+    hipMemcpy(di2, i2, sizeof(i2), hipMemcpyHostToDevice);
+    hipMemcpy(do2, o2, sizeof(o2), hipMemcpyHostToDevice);
+    probe<<<1, 64>>>(x, rows, pitch, di2, do2, d2, m);
+    hipDeviceSynchronize();
+    hipMemcpy(r2, d2, sizeof(r2), hipMemcpyDeviceToHost);
+    float chk[176];
+    hipMemcpy(chk, reinterpret_cast<char*>(x) + int64_t(7999999) * pitch, pitch, hipMemcpyDeviceToHost);
+    printf("last row via memcpy: f0 %.4f f174 %.4f f175 %.4f\n", chk[0], chk[174], chk[175]);
+    for (int i = 0; i < m; ++i) printf("  index %d offset %d -> %.6f\n", i2[i], o2[i], r2[i]);
+  }
   const char* what[n] = {"row 3 off 4", "row 6.1M off 660 (index*stride > 4 GiB)", "last row off 700",
                          "row 5000001 off 0", "index == num_records", "index 0x7fffffff",
                          "row 3 offset == stride", "last row offset > stride"};

@@ -220,3 +220,28 @@ def test_c3_full_size_49_snapshots_match_oracle(elliptic, golden):
     assert_close(gout.cpu(), rout, what="C3 whole-graph out")
     assert_close(ghid.cpu(), rhid, what="C3 whole-graph hidden")
     assert worst < 1e-4
+
+
+def test_c1_two_layer_eval_forward_full_graph(elliptic, golden):
+    """C1 as configured (BASELINE.json configs[0]; gat.py:60-96 with
+    num_layers=2): GAT(165, 64, 1, num_layers=2) in eval mode on the whole
+    203,769-node graph, with the shipped checkpoint's first two layers (and
+    its head), against oracle.GATRef on the CPU.  (the
+    bench leg checked this after timing only.)"""
+    from gfd.models import GAT
+    from oracle import GATRef
+    arr = golden("elliptic_small.npz")
+    sd = {k: v for k, v in state_dict_from(arr, "gat.").items()
+          if not k.startswith(("gat_layers.2.", "batch_norms.2."))}
+    m = GAT(in_channels=165, hidden_channels=64, out_channels=1, num_layers=2, dropout=0.2)
+    m.load_state_dict(sd, strict=True)
+    ref = GATRef(165, 64, 1, num_layers=2, dropout=0.2)
+    ref.load_state_dict({k: v.clone() for k, v in sd.items()}, strict=True)
+    m, ref = m.to(DEV).eval(), ref.eval()
+    x = torch.from_numpy(elliptic["x"])
+    ei = torch.from_numpy(elliptic["edge_index"])
+    with torch.no_grad():
+        got = m(x.to(DEV), ei.to(DEV)).cpu()
+        want = ref(x, ei)
+    assert got.shape == want.shape == (203_769, 1)
+    assert_close(got, want, what="C1 2-layer eval logits (full graph)")
