@@ -113,7 +113,7 @@ __device__ __forceinline__ void mfma3(f32x4& acc, f16x8 ahi, f16x8 alo, f16x8 bh
 // work, 1 of it waiting for the step's rows, 2 MFMA-step work, 3 barrier after
 // an aggregation step, 4 barrier after an MFMA step, 5 aggregation steps,
 // 6 MFMA steps (scripts/prof_light_pair.py)
-__device__ unsigned long long g_lprof[2][8];
+__device__ unsigned long long g_lprof[2][16];
 #endif
 
 size_t light_pair_smem(int Fp, int lo) {
@@ -211,14 +211,11 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
     return e1 < 0 ? 0 : e1 - e0;
   };
 
-  // a pass's rows for the next tile (lane <-> its slot's three features):
-  // features 0, 1 of round k in xa[p][k], feature 2 of rounds 2 i, 2 i + 1 in
-  // xb[p][i] -- register PAIRS, so the packed FMAs broadcast either half by
-  // op_sel (single floats would each take an aligned pair)
 #ifdef GFD_LP_PROF
   unsigned long long pw = 0ull;  // cycles waiting for rows (aggregation)
+  unsigned long long pv[4] = {0ull, 0ull, 0ull, 0ull};  // softmax, aggregate, rows issue, logits
 #endif
-  f32x2 xa[2][kLR], xb[2][(kLR + 1) / 2];
+  float xr[2][kLR][3];  // a pass's rows for the next tile (lane <-> its slot's three features)
   Logits lg;            // logits of the wave's next softmax
   int Cq[4];            // records of tiles v .. v + 3 (of the wave's next aggregation v)
 
@@ -233,23 +230,27 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
     const int R = max(na, nb), nmin = min(na, nb);
     const int nl = hf ? nb : na;
     const char* xl = reinterpret_cast<const char*>(x) + (fg + li) * eb;
+    // all sources of the pass first (one LDS wait), then the row loads
+    int jr[kLR];
+#pragma unroll
+    for (int k = 0; k < kLR; ++k)
+      if (k < R) jr[k] = __builtin_amdgcn_ds_bpermute((8 * q + k) << 2, Cn);
 #pragma unroll
     for (int k = 0; k < kLR; ++k) {
       if (k < R) {
-        const int j = __builtin_amdgcn_ds_bpermute((8 * q + k) << 2, Cn);
         // the lane's first feature of row j (64-bit: x exceeds the 4 GiB a
         // buffer descriptor reaches -- scripts/sbuf_probe.hip)
         const typename XT::T* ra = reinterpret_cast<const typename XT::T*>(
-            xl + uint64_t(uint32_t(j)) * uint64_t(uint32_t(pitch)));
+            xl + uint64_t(uint32_t(jr[k])) * uint64_t(uint32_t(pitch)));
         float x0 = 0.f, x1 = 0.f, x2 = 0.f;
         if (k < nmin || k < nl) {  // (uniform, or this half's slot has message k)
           x0 = xcvt(ra[0]);
           x1 = xcvt(ra[32]);
           if (v2) x2 = xcvt(ra[64]);
         }
-        xa[p][k] = f32x2{x0, x1};
-        if (k & 1) xb[p][k >> 1].y = x2;
-        else xb[p][k >> 1].x = x2;
+        xr[p][k][0] = x0;
+        xr[p][k][1] = x1;
+        xr[p][k][2] = x2;
       }
     }
   };
@@ -322,38 +323,40 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
       pw += __builtin_amdgcn_s_memtime() - w0;
     }
 #endif
-    f32x2 z[4][3];
+    // plain FMAs, not v_pk_fma_f32: beside the partner wave's MFMAs a packed
+    // FMA costs far more than two plain ones (MI355X_MICROARCH.md, fillers
+    // beside MFMAs).  Same arithmetic per element.  The next round's weights
+    // are read one round ahead.
+    float z[H][3];
+    f32x4 w0 = *reinterpret_cast<const f32x4*>(pr), w1 = *reinterpret_cast<const f32x4*>(pr + 4);
 #pragma unroll
     for (int k = 0; k < kLR; ++k) {
       if (k == 0 || k < R) {
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(pr + 8 * k);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(pr + 8 * k + 4);
-        const f32x2 p2[4] = {f32x2{a0.x, a0.y}, f32x2{a0.z, a0.w}, f32x2{a1.x, a1.y},
-                             f32x2{a1.z, a1.w}};
-        const f32x2 x01 = xa[p][k], x2p = xb[p][k >> 1];
-        const f32x2 xx[3] = {f32x2{x01.x, x01.x}, f32x2{x01.y, x01.y},
-                             (k & 1) ? f32x2{x2p.y, x2p.y} : f32x2{x2p.x, x2p.x}};
+        const float pk[H] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        if (k + 1 < kLR && k + 1 < R) {
+          w0 = *reinterpret_cast<const f32x4*>(pr + 8 * (k + 1));
+          w1 = *reinterpret_cast<const f32x4*>(pr + 8 * (k + 1) + 4);
+        }
 #pragma unroll
-        for (int hp = 0; hp < 4; ++hp)
+        for (int h = 0; h < H; ++h)
 #pragma unroll
           for (int m = 0; m < 3; ++m)
-            z[hp][m] = k == 0 ? p2[hp] * xx[m] : __builtin_elementwise_fma(p2[hp], xx[m], z[hp][m]);
-        // (the round's weights are read where used: no registers for the others)
+            z[h][m] = k == 0 ? pk[h] * xr[p][k][m] : fmaf(pk[h], xr[p][k][m], z[h][m]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (erg == 127) {  // kernel-uniform: a scale for this row's half from its own max |z|
       float zm = 0.f;
 #pragma unroll
-      for (int hp = 0; hp < 4; ++hp)
+      for (int h = 0; h < H; ++h)
 #pragma unroll
-        for (int m = 0; m < 3; ++m) zm = fmaxf(zm, fmaxf(fabsf(z[hp][m].x), fabsf(z[hp][m].y)));
+        for (int m = 0; m < 3; ++m) zm = fmaxf(zm, fabsf(z[h][m]));
       const int er = scale_exp(max_half32(zm));
       const float sc = ldexpf(1.0f, er);
 #pragma unroll
-      for (int hp = 0; hp < 4; ++hp)
+      for (int h = 0; h < H; ++h)
 #pragma unroll
-        for (int m = 0; m < 3; ++m) z[hp][m] *= f32x2{sc, sc};
+        for (int m = 0; m < 3; ++m) z[h][m] *= sc;
       if (li == 0) rsc[(g * 2 + par) * kTile + r] = ldexpf(1.0f, -er);
     }
     _Float16* zh = Zh + (g * kTile + r) * ZSH;
@@ -363,8 +366,9 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
       union { f16x8 v; f16x2 p[4]; uint32_t u[4]; } a, b;
 #pragma unroll
       for (int hp = 0; hp < 4; ++hp) {
-        a.p[hp] = __builtin_convertvector(z[hp][m], f16x2);
-        b.u[hp] = split_lo(z[hp][m], a.u[hp]);
+        const f32x2 zz = f32x2{z[2 * hp][m], z[2 * hp + 1][m]};
+        a.p[hp] = __builtin_convertvector(zz, f16x2);
+        b.u[hp] = split_lo(zz, a.u[hp]);
       }
       if (m < 2 || w2) {
         const int f = 32 * m + li;
@@ -434,7 +438,20 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
   // both passes; group 1 -- both passes of tile v, then the weights of its
   // slots of tile v + 1 (P holds one tile: each slot's weights are read by
   // waves (0, ct) and (1, ct) before group 1 replaces them)
+#ifdef GFD_LP_PROF
+#define GFD_LP_STAMP(i)                                          \
+  do {                                                           \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
+    pv[i] += _t - tv;                                            \
+    tv = _t;                                                     \
+  } while (0)
+#else
+#define GFD_LP_STAMP(i) do {} while (0)
+#endif
   auto valu_step = [&](int64_t v) {
+#ifdef GFD_LP_PROF
+    unsigned long long tv = __builtin_amdgcn_s_memtime();
+#endif
     Cq[3] = rec_load(v + 3);
     if (g == 0) {
       softmax(Cq[0], v);
@@ -444,13 +461,18 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
+    GFD_LP_STAMP(0);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       if (v >= 0) aggregate(Cq[0], v, p);
+      GFD_LP_STAMP(1);
       rows_issue(Cq[1], v + 1, p);
+      GFD_LP_STAMP(2);
     }
     if (g == 1 && v + 1 < nv) softmax(Cq[1], v + 1);
+    GFD_LP_STAMP(0);
     logits_issue(g == 0 ? Cq[1] : Cq[2], v + 1 + g);
+    GFD_LP_STAMP(3);
   };
   auto rotate = [&]() {
     Cq[0] = Cq[1];
@@ -520,6 +542,8 @@ __global__ void __launch_bounds__(kLW * 64, 2) k_light_pair(
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) atomicAdd(&g_lprof[g][i], pc[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_lprof[g][8 + i], pv[i]);
   }
 #endif
 }
@@ -579,7 +603,7 @@ gfd_status launch_light_pair(const AggArgs& a, const PackLayout& L, bool to_end,
 extern "C" int gfd_lprof_read(unsigned long long* out16, int reset) {
   if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_lprof), sizeof(g_lprof)) != hipSuccess) return 1;
   if (reset) {
-    static const unsigned long long zero[2][8] = {};
+    static const unsigned long long zero[2][16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_lprof), zero, sizeof(zero)) != hipSuccess) return 1;
   }
   return 0;

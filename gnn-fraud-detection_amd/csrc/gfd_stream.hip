@@ -60,6 +60,10 @@ constexpr int kSWaves = 8;
 #ifndef GFD_LIGHT_PAIR
 #define GFD_LIGHT_PAIR 0
 #endif
+// s_setprio 1 once for one half of the block (1: waves 4-7, 2: waves 0-3)
+#ifndef GFD_STREAM_SETPRIO
+#define GFD_STREAM_SETPRIO 0
+#endif
 #ifndef GFD_STREAM_ZPAD
 #define GFD_STREAM_ZPAD 8
 #endif
@@ -486,6 +490,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     else WL[(wave * LO + (u - NR)) * 64 + lane] = vl;
   }
   if (nv == 0) return;  // uniform per block: no barrier below is reached by anyone
+#if GFD_STREAM_SETPRIO == 1
+  // static priority for the second-dispatched half (waves 4-7), once, before
+  // the loop (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#elif GFD_STREAM_SETPRIO == 2
+  if (wave < 4) __builtin_amdgcn_s_setprio(1);
+#endif
 
   SlotRec n0, n1;
   constexpr int NL = nl_of<LIGHT, XT>();  // rows issued one tile ahead per slot

@@ -26,7 +26,7 @@ def main():
     lib = _lib.load()
     rd = lib.gfd_lprof_read
     rd.argtypes = [ct.c_void_p, ct.c_int]
-    buf = (ct.c_ulonglong * 16)()
+    buf = (ct.c_ulonglong * 32)()
     for _ in range(2):
         layer.step()
     torch.cuda.synchronize()
@@ -36,12 +36,16 @@ def main():
     torch.cuda.synchronize()
     rd(buf, 0)
     for g in (0, 1):
-        v = [buf[8 * g + i] for i in range(7)]
+        v = [buf[16 * g + i] for i in range(7)]
+        w = [buf[16 * g + 8 + i] for i in range(4)]
         ns, nm = max(v[5], 1), max(v[6], 1)
         print(f"{'C5' if c5 else 'C4'} group {g}: aggregation step {v[0] / ns:.0f} cyc "
               f"(rows wait {v[1] / ns:.0f}), barrier after it {v[3] / ns:.0f}; "
               f"MFMA step {v[2] / nm:.0f} cyc, barrier after it {v[4] / nm:.0f}  "
               f"[{v[5]} / {v[6]} wave-steps]")
+        print("   aggregation step: " + ", ".join(
+            f"{n} {x / ns:.0f}" for n, x in zip(("softmax", "aggregate (2 passes)", "rows issue",
+                                                 "logits + records"), w)))
 
 
 if __name__ == "__main__":
