@@ -540,10 +540,6 @@ gfd_status launch_hubs(const AggArgs& a, const PackLayout& L, hipStream_t stream
 // tile stages; GFD_ERR_UNSUPPORTED when the configuration is outside the kernel's set
 gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end, hipStream_t stream);
-// the paired-phase light kernel (gfd_light.hip): fp32 rows, 64 + Fp / 2 <= F <= 168
-bool light_pair_supported(const AggArgs& a, const PackLayout& L);
-gfd_status launch_light_pair(const AggArgs& a, const PackLayout& L, bool to_end,
-                             hipStream_t stream);
 gfd_status launch_lone(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_fused(const AggArgs& a, const PackLayout& L, hipStream_t stream);
 gfd_status launch_logits(const void* x, int xdt, int64_t rows, int F, int64_t ldx,

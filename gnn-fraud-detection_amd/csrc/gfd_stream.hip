@@ -54,18 +54,17 @@ namespace {
 #define GFD_HOUT(ep) (EPI && ep.hout)
 
 constexpr int kSWaves = 8;
-// Z tile row pad (halves): 8 gives the A-fragment ds_read_b128 reads a 2-way
-// bank conflict in one of their 16-lane groups, 16 none (scripts/bank_pad.py)
-// fp32 light rows with 64 + Fp / 2 <= F go to the paired-phase kernel (gfd_light.hip)
-#ifndef GFD_LIGHT_PAIR
-#define GFD_LIGHT_PAIR 0
-#endif
-// s_setprio 1 once for one half of the block (1: waves 4-7, 2: waves 0-3)
+// s_setprio 1 once for one half of the block (1: waves 4-7, 2: waves 0-3):
+// within box noise either way (C4 13.14-13.16 / 13.00-13.03 vs 13.09-13.19 ms,
+// profiles/r6_stream_knobs_ab.txt), off
 #ifndef GFD_STREAM_SETPRIO
 #define GFD_STREAM_SETPRIO 0
 #endif
+// Z tile row pad (halves): 8 gives the A-fragment ds_read_b128 reads a 2-way
+// bank conflict in one of their 16-lane groups, 16 none (scripts/bank_pad.py;
+// C4 13.09 / 13.19 -> 12.99 / 13.00 ms, profiles/r6_stream_knobs_ab.txt)
 #ifndef GFD_STREAM_ZPAD
-#define GFD_STREAM_ZPAD 8
+#define GFD_STREAM_ZPAD 16
 #endif
 // Light slots: message weights broadcast through LDS (fma_k_lds: 2 broadcast
 // reads per message instead of 8 v_readlane; the light kernel's VALU count
@@ -777,9 +776,6 @@ gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols || !p.class_split) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-#if GFD_LIGHT_PAIR
-  if (light_pair_supported(a, L)) return launch_light_pair(a, L, to_end, stream);
-#endif
   return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, stream)
                                  : launch_stream_x<XF32, true>(a, L, to_end, stream);
 }

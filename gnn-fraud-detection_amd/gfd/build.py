@@ -45,11 +45,7 @@ BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-
 #   checked -- the bounds-checked diagnostic build (gfd_check.h)
 SHIPPED_VARIANTS = {"checked": ["-DGFD_CHECKED"]}
 # Per-source flags: {"file.hip": [flags]}
-SOURCE_FLAGS = {
-    # the paired-phase light kernel: plain f32 FMAs, never SLP-packed into
-    # v_pk_fma_f32 (expensive beside the partner wave's MFMAs)
-    "gfd_light.hip": ["-fno-slp-vectorize"],
-}
+SOURCE_FLAGS = {}
 
 
 def lib_path(variant: str = "") -> str:
