@@ -21,6 +21,15 @@ constexpr float kSoftmaxEps = 1e-16f;  // PyG utils.softmax denominator epsilon
 #define GFD_LIGHT_MAX 6
 #endif
 constexpr int kLightMax = GFD_LIGHT_MAX;
+// Messages of the largest destination of the "short light" sub-class: the
+// light tiles whose slots all have at most this many messages run a kernel
+// instance that prefetches only that many rows per slot, and spends the
+// registers so freed on a deeper A-fragment read-ahead (gfd_stream.hip).  The
+// plan's third class boundary (k_slot_desc) uses the same bound.
+#ifndef GFD_LIGHT_LO
+#define GFD_LIGHT_LO 3
+#endif
+constexpr int kLightLo = GFD_LIGHT_LO;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

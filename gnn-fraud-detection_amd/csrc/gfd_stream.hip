@@ -83,12 +83,24 @@ constexpr int kSWaves = 8;
 #ifndef GFD_GENERAL_AP
 #define GFD_GENERAL_AP 1
 #endif
+// short light tiles (every slot at most kLightLo messages: LIGHT = 2): kLightLo
+// rows per slot in flight instead of kLightMax, so the A fragments can be read
+// further ahead
+#ifndef GFD_LIGHT_LO_AP
+#define GFD_LIGHT_LO_AP 2
+#endif
+#ifndef GFD_LIGHT_LO_AP_BF16
+#define GFD_LIGHT_LO_AP_BF16 2
+#endif
 // A-fragment k-steps read ahead in the MFMA loop (general; light fp32 / bf16
 // rows).  Light fp32: 1 keeps the kernel spill-free with 6 rows per slot in
 // flight (C4 light 6.73 -> 6.22 ms against 2); light bf16: 2 (C5 33.3 vs 33.7 ms)
-template <bool LIGHT, typename XT>
+// LIGHT: 0 general tiles, 1 light tiles (2..kLightMax messages), 2 short
+// light tiles (at most kLightLo)
+template <int LIGHT, typename XT>
 constexpr int ap_of() {
-  return LIGHT ? (XT::kBytes == 2 ? GFD_LIGHT_AP_BF16 : GFD_LIGHT_AP) : GFD_GENERAL_AP;
+  return LIGHT == 2 ? (XT::kBytes == 2 ? GFD_LIGHT_LO_AP_BF16 : GFD_LIGHT_LO_AP)
+       : LIGHT ? (XT::kBytes == 2 ? GFD_LIGHT_AP_BF16 : GFD_LIGHT_AP) : GFD_GENERAL_AP;
 }
 // x rows of a general slot issued one tile ahead (the rest of batch 0 is
 // issued when its aggregation starts).  fp32 rows: none -- the kernel is then
@@ -101,9 +113,10 @@ constexpr int ap_of() {
 #ifndef GFD_GENERAL_NL_BF16
 #define GFD_GENERAL_NL_BF16 4
 #endif
-template <bool LIGHT, typename XT>
+template <int LIGHT, typename XT>
 constexpr int nl_of() {
-  return LIGHT ? kLightMax : (XT::kBytes == 2 ? GFD_GENERAL_NL_BF16 : GFD_GENERAL_NL_F32);
+  return LIGHT == 2 ? kLightLo
+       : LIGHT ? kLightMax : (XT::kBytes == 2 ? GFD_GENERAL_NL_BF16 : GFD_GENERAL_NL_F32);
 }
 
 #ifdef GFD_PROF
@@ -151,7 +164,7 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
 // window (general) and the ring record; part 1 + k = x row k.  Issued
 // unconditionally (past the last slot: clamped, ignored records), so no
 // branch joins in-flight loads.
-template <int PART, typename XT, int KF, bool LIGHT, int NRW>
+template <int PART, typename XT, int KF, int LIGHT, int NRW>
 __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW>& q,
                                               const void* __restrict__ x, int64_t ldx, int F,
                                               const int32_t* __restrict__ col,
@@ -187,31 +200,30 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW
   }
 }
 
-// z = sum of the first kmax (2 .. kLightMax, wave-uniform) rows, one
-// straight-line block per count
-template <int KF>
-__device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[kLightMax][KF],
-                                          float p, int kmax) {
-  static_assert(kLightMax >= 4 && kLightMax <= 7, "light slots: 4 .. 7 messages");
-  if (kmax <= 2) fma_k<KF, 2>(z, xv, p);
-  else if (kmax == 3) fma_k<KF, 3>(z, xv, p);
-  else if (kLightMax == 4 || kmax == 4) fma_k<KF, 4>(z, xv, p);
-  else if (kLightMax == 5 || kmax == 5) fma_k<KF, (kLightMax >= 5 ? 5 : 4)>(z, xv, p);
-  else if (kLightMax == 6 || kmax == 6) fma_k<KF, (kLightMax >= 6 ? 6 : 4)>(z, xv, p);
-  else fma_k<KF, kLightMax>(z, xv, p);
+// z = sum of the first kmax (2 .. NR, wave-uniform) rows, one straight-line
+// block per count (K = 2 .. NR)
+template <int KF, int NR, int K = 2>
+__device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[NR][KF], float p,
+                                          int kmax) {
+  static_assert(NR >= 2 && NR <= 7, "light slots: 2 .. 7 messages");
+  if constexpr (K >= NR) {
+    fma_k<KF, NR>(z, xv, p);
+  } else {
+    if (kmax <= K) fma_k<KF, K>(z, xv, p);
+    else light_fma<KF, NR, K + 1>(z, xv, p, kmax);
+  }
 }
 
 // light_fma with the weights from the wave's LDS buffer (fma_k_lds)
-template <int KF>
-__device__ __forceinline__ void light_fma_lds(f32x2 (&z)[4][KF],
-                                              const float (&xv)[kLightMax][KF],
+template <int KF, int NR, int K = 2>
+__device__ __forceinline__ void light_fma_lds(f32x2 (&z)[4][KF], const float (&xv)[NR][KF],
                                               const float* __restrict__ ab, int kmax) {
-  if (kmax <= 2) fma_k_lds<KF, 2>(z, xv, ab);
-  else if (kmax == 3) fma_k_lds<KF, 3>(z, xv, ab);
-  else if (kLightMax == 4 || kmax == 4) fma_k_lds<KF, 4>(z, xv, ab);
-  else if (kLightMax == 5 || kmax == 5) fma_k_lds<KF, (kLightMax >= 5 ? 5 : 4)>(z, xv, ab);
-  else if (kLightMax == 6 || kmax == 6) fma_k_lds<KF, (kLightMax >= 6 ? 6 : 4)>(z, xv, ab);
-  else fma_k_lds<KF, kLightMax>(z, xv, ab);
+  if constexpr (K >= NR) {
+    fma_k_lds<KF, NR>(z, xv, ab);
+  } else {
+    if (kmax <= K) fma_k_lds<KF, K>(z, xv, ab);
+    else light_fma_lds<KF, NR, K + 1>(z, xv, ab, kmax);
+  }
 }
 
 // A slot with at most kLightMax messages (all rows prefetched), not a hub
@@ -219,8 +231,8 @@ __device__ __forceinline__ void light_fma_lds(f32x2 (&z)[4][KF],
 // one, so the head-mean shortcut of k_lone does not apply): straight-line
 // code, the softmax sum and reciprocal independent of the FMA block.  kmax:
 // messages to run (wave-uniform, >= n).
-template <int KF>
-__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLightMax>& q, int kmax,
+template <int KF, int NR>
+__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, NR>& q, int kmax,
                                          float slope, float dp, uint64_t seed, int Fp,
                                          float* __restrict__ stats,
                                          _Float16* __restrict__ zh, _Float16* __restrict__ zl,
@@ -258,17 +270,17 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLight
     const float ps = pd * (inv * ldexpf(1.0f, erg));
 #if GFD_LIGHT_ALDS
     ab[lane] = ps;  // this wave's own buffer: its LDS operations run in order
-    light_fma_lds<KF>(z, q.xv, ab, kmax);
+    light_fma_lds<KF, NR>(z, q.xv, ab, kmax);
 #else
-    light_fma<KF>(z, q.xv, ps, kmax);
+    light_fma<KF, NR>(z, q.xv, ps, kmax);
 #endif
     split_zrow<KF>(z, hi, lo);
   } else {
 #if GFD_LIGHT_ALDS
     ab[lane] = pd;
-    light_fma_lds<KF>(z, q.xv, ab, kmax);
+    light_fma_lds<KF, NR>(z, q.xv, ab, kmax);
 #else
-    light_fma<KF>(z, q.xv, pd, kmax);
+    light_fma<KF, NR>(z, q.xv, pd, kmax);
 #endif
     er = pack_zrow<KF>(z, inv, erg, hi, lo);
   }
@@ -289,6 +301,9 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, kLight
 //    the end of the current one (one memory round trip per batch; a col ->
 //    st -> rows chain would be three).
 //  * hub rows: the merged, normalised z of k_hub_fin.
+//  * xa / xb (8 rows of a batch) belong to the caller: the wave's two slots
+//    share them, which keeps the bf16 instance (4 rows a tile ahead) spill-free
+//    (C5 general stage 34.4 -> 25.9 ms; profiles/r6p_general_rows_ab.txt).
 template <typename XT, int KF, int NRW, int NRA>
 __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
                                            const SlotRows<KF, NRA>& q, const void* __restrict__ x,
@@ -298,17 +313,35 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
                                            uint64_t seed, const float* __restrict__ zhub,
                                            float* __restrict__ stats, _Float16* __restrict__ zh,
                                            _Float16* __restrict__ zl, float* __restrict__ rsc,
-                                           int* __restrict__ rid, int r, int erg, int lane) {
+                                           int* __restrict__ rid, int r, int erg, int lane,
+                                           float (&xa)[4][KF], float (&xb)[4][KF]) {
   const int4 d = uni4(ring->d);
   const int j0 = ring->j[lane >> 3];
   const int h = lane & 7, kk = lane >> 3;
+  // batch 0 of a slot: rows 0..3 (4..7 when it has more than 4 messages)
+  auto issue0 = [&](int ja, int na) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(ja, 8 * k), ldx), F, lane, k < na,
+                       xa[k]);
+    if (na > 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(ja, 8 * (4 + k)), ldx), F, lane,
+                         4 + k < na, xb[k]);
+    }
+  };
   f32x2 z[4][KF];
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int qq = 0; qq < KF; ++qq) z[g][qq] = f32x2{0.f, 0.f};
   float inv = 1.0f;
-  if (d.x >= 0 && d.w >= 0) {  // hub: merged row (already normalised)
+  if (d.x < 0) {  // past the last destination
+    if (lane == 0) rid[r] = -1;
+    return;
+  }
+  if (d.w >= 0) {  // hub: merged row (already normalised)
     const float* src = zhub + int64_t(d.w) * (H * Fp);
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -317,25 +350,13 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
         const int f = lane + 64 * qq;
         if (f < Fp) z[g][qq] = f32x2{src[2 * g * Fp + f], src[(2 * g + 1) * Fp + f]};
       }
-  } else if (d.x >= 0) {
+  } else {
     const int e0 = d.y, e1 = d.z;
     const int n = e1 - e0;
-    float xa[4][KF], xb[4][KF];
     const float keep = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
     float m, l;
     {  // batch 0
-      if constexpr (NRW == 0) {  // rows 0..7 issued here, before the softmax
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * k), ldx), F, lane, k < n,
-                           xa[k]);
-        if (n > 4) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), ldx), F,
-                             lane, 4 + k < n, xb[k]);
-        }
-      }
+      if constexpr (NRW == 0) issue0(j0, n);  // rows 0..7 issued here, before the softmax
       const bool valid = kk < n;
       const float v = leaky01(q.sj + q.th, slope);
       m = max_xor8_16_32(valid ? v : -INFINITY);
@@ -411,10 +432,6 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
     }
     inv = __builtin_amdgcn_rcpf(l + kSoftmaxEps);
   }
-  if (d.x < 0) {
-    if (lane == 0) rid[r] = -1;
-    return;
-  }
   f16x8 hi[KF], lo[KF];
   const int er = pack_zrow<KF>(z, inv, erg, hi, lo);
   write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
@@ -424,7 +441,7 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
   }
 }
 
-template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT, bool EPI>
+template <typename XT, int KF, int KHM, int LO, bool EXACT, int LIGHT, bool EPI>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t num_dst, const int4* __restrict__ desc,
@@ -456,11 +473,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   const int64_t G = gridDim.x;
   const int64_t t0 = blockIdx.x;
   // general tiles: [0, ceil(split[0] / 16)), every tile without a split;
-  // light tiles: [ceil(split[0] / 16), ceil(split[1] / 16)) (to_end: up to the
-  // last tile, when k_lone does not run); this block takes tiles t0 + v G
+  // light tiles: [ceil(split[0] / 16), ceil(split[2] / 16)); short light
+  // tiles: [ceil(split[2] / 16), ceil(split[1] / 16)) (to_end: up to the last
+  // tile, when k_lone does not run); this block takes tiles t0 + v G
   const int64_t all = (num_dst + kTile - 1) / kTile;
-  const int64_t tb = LIGHT ? (split[0] + kTile - 1) / kTile : 0;
-  const int64_t te = LIGHT ? ((to_end ? num_dst : split[1]) + kTile - 1) / kTile
+  const int64_t tb = LIGHT ? (split[LIGHT == 2 ? 2 : 0] + kTile - 1) / kTile : 0;
+  const int64_t te = LIGHT == 2 ? ((to_end ? num_dst : split[1]) + kTile - 1) / kTile
+                   : LIGHT ? (split[2] + kTile - 1) / kTile
                            : (split ? (split[0] + kTile - 1) / kTile : all);
   const int64_t nv = t0 < te - tb ? (te - tb - 1 - t0) / G + 1 : 0;
   // light, not to the end: the slots of the last tile past split[1] are lone
@@ -534,10 +553,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       sl_light<KF>(db, d1, kmax, slope, dp, seed, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid,
                    r1, erg, ab + 64, lane);
     } else {
+      float xa[4][KF], xb[4][KF];  // the two slots' batch registers (sl_general)
       sl_general<XT, KF, NL, NA>(rg + r0, d0, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
-                                 stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane);
+                                 stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane, xa, xb);
       sl_general<XT, KF, NL, NA>(rg + r1, d1, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
-                                 stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg, lane);
+                                 stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg, lane, xa, xb);
     }
   };
   aggregate(0);
@@ -712,7 +732,7 @@ size_t stream_smem(int Fp, int lo) {
          sizeof(int) * 2 * kTile;
 }
 
-template <typename XT, int KF, int KHM, int LO, bool EXACT, bool LIGHT>
+template <typename XT, int KF, int KHM, int LO, bool EXACT, int LIGHT>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
   const bool epi = a.ep.ab != nullptr || a.ep.hout != nullptr;
@@ -742,7 +762,7 @@ gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
 // Instance for this K: KH = KS / 2 k-steps per wave, at most KHM = 8 / 16 / 21
 // for one / two / three feature chunks (F <= 64 / 128 / 168).  KF = 3 keeps
 // W_lo of 8 k-steps per wave in LDS.
-template <typename XT, bool LIGHT>
+template <typename XT, int LIGHT>
 gfd_status launch_stream_x(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
   const int KF = kf_for(a.F);
@@ -767,8 +787,8 @@ gfd_status launch_general(const AggArgs& a, const PackLayout& L, hipStream_t str
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, false>(a, L, false, stream)
-                                 : launch_stream_x<XF32, false>(a, L, false, stream);
+  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, 0>(a, L, false, stream)
+                                 : launch_stream_x<XF32, 0>(a, L, false, stream);
 }
 
 gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
@@ -776,8 +796,12 @@ gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
   const gfd_plan& p = a.plan;
   if (!p.slot_desc || !p.slot_cols || !p.class_split) return GFD_ERR_UNSUPPORTED;
   if (!(a.slope >= 0.f && a.slope <= 1.f)) return GFD_ERR_UNSUPPORTED;  // leaky01
-  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, true>(a, L, to_end, stream)
-                                 : launch_stream_x<XF32, true>(a, L, to_end, stream);
+  // the light tiles, then the short light tiles (two persistent launches)
+  const gfd_status st = a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, 1>(a, L, to_end, stream)
+                                                : launch_stream_x<XF32, 1>(a, L, to_end, stream);
+  if (st != GFD_OK) return st;
+  return a.xdt == GFD_DTYPE_BF16 ? launch_stream_x<XBF16, 2>(a, L, to_end, stream)
+                                 : launch_stream_x<XF32, 2>(a, L, to_end, stream);
 }
 
 }  // namespace fwd

@@ -71,7 +71,8 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 class Plan:
     """Execution plan of one destination range (``gfd_plan``): the tile order
     (destinations by descending message count), the hub split and the slot
-    class boundaries (``class_split``: first light slot, first lone slot)."""
+    class boundaries (``class_split``: first light slot, first lone slot, first
+    short-light slot -- at most 3 messages, their own tile kernel instance))."""
     num_dst: int
     row_order: Optional[torch.Tensor]
     slot_desc: Optional[torch.Tensor]
@@ -108,7 +109,7 @@ class Plan:
         """(first light slot, first lone slot) on the host (syncs)."""
         if self.class_split is None:
             return self.num_dst, self.num_dst
-        a, b = self.class_split.tolist()
+        a, b = self.class_split.tolist()[:2]
         return int(a), int(b)
 
 
@@ -139,7 +140,7 @@ def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THR
         slot_desc = torch.empty(4 * n, dtype=torch.int32, device=dev)
         if col is not None:
             slot_cols = torch.empty(8 * n, dtype=torch.int32, device=dev)
-            class_split = torch.empty(2, dtype=torch.int64, device=dev)
+            class_split = torch.empty(3, dtype=torch.int64, device=dev)
         _lib.call("gfd_plan_desc", rowptr.data_ptr(), _lib.ptr(col), n, _lib.ptr(row_order),
                   hub_rank.data_ptr() if nh > 0 else None, slot_desc.data_ptr(),
                   _lib.ptr(slot_cols), _lib.ptr(class_split), stream)
