@@ -584,7 +584,8 @@ def measure(args, dev, rank, world, config):
                           "RCCL all-gather-v of the [N, 8] source logits + max|x| all-reduce"),
              "hubs": "k_hub_partial + k_hub_fin",
              "general": "k_stream<general> (hub rows, 7+ messages)",
-             "light": "k_stream<light> (2-6 messages)",
+             "light": "k_stream<light> (2-6 messages: the 4-6-message tiles, then the "
+                      "short tiles of at most 3 -- two launches)",
              "lone": "k_lone (self-loop-only rows)"}
     pmc = load_pmc(args.pmc, f"{config}:{dom}:N={N}:E={E}:F={F}:world={world}")
     workload = (f"{config.upper()} power-law N={N} E={E} F={F} gamma={args.gamma} "

@@ -141,6 +141,43 @@ __device__ __forceinline__ void row_regs(const char* xr, int F, int lane, bool o
   }
 }
 
+// Lane layouts of a gathered row held in registers by the tile kernels.
+//  RowL<XT, KF, false>: KF registers, register q = feature lane + 64 q (row_regs).
+//  RowL<XBF16, 3, true>: bf16 rows with 128 < F <= 192 whose starts are 4-B
+//    aligned: 2 registers -- the raw bf16 pair of features 2 lane, 2 lane + 1
+//    (one 4-B load) and feature 128 + lane (one 2-B load) -- so a row costs 2
+//    VGPRs instead of 3.  Aggregation chunk q is then feature feat(q, lane).
+// x(v, q): the fp32 value of chunk q of a held row.
+template <typename XT, int KF, bool PR>
+struct RowL {
+  static constexpr int W = KF;
+  __device__ static __forceinline__ int feat(int q, int lane) { return lane + 64 * q; }
+  __device__ static __forceinline__ void load(const char* xr, int F, int lane, bool ok,
+                                              float (&v)[W]) {
+    row_regs<XT, KF>(xr, F, lane, ok, v);
+  }
+  __device__ static __forceinline__ float x(const float (&v)[W], int q) { return v[q]; }
+};
+template <>
+struct RowL<XBF16, 3, true> {
+  static constexpr int W = 2;
+  __device__ static __forceinline__ int feat(int q, int lane) {
+    return q < 2 ? 2 * lane + q : 128 + lane;
+  }
+  __device__ static __forceinline__ void load(const char* xr, int F, int lane, bool ok,
+                                              float (&v)[W]) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(xr), 0, __builtin_amdgcn_readfirstlane(ok ? F * 2 : 0), 0x00020000);
+    v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+    v[1] = __uint_as_float(uint32_t(__builtin_amdgcn_raw_buffer_load_b16(rs, 256 + lane * 2, 0, 0))
+                           << 16);
+  }
+  __device__ static __forceinline__ float x(const float (&v)[W], int q) {
+    return q == 0 ? __uint_as_float(__float_as_uint(v[0]) << 16)
+         : q == 1 ? __uint_as_float(__float_as_uint(v[0]) & 0xffff0000u) : v[1];
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Cross-lane helpers: DPP row rotates + gfx950 permlane swaps (a few VALU
 // cycles each instead of a ds_bpermute round trip per step).
@@ -280,13 +317,13 @@ __device__ __forceinline__ void split_zrow(const f32x2 (&z)[4][KF], f16x8 (&hi)[
 }
 
 // Store a packed row into a Z tile (one 16-B write per feature and plane).
-template <int KF>
+template <int KF, typename RL = RowL<XF32, KF, false>>
 __device__ __forceinline__ void write_zrow(const f16x8 (&hi)[KF], const f16x8 (&lo)[KF], int Fp,
                                            int lane, _Float16* __restrict__ zh,
                                            _Float16* __restrict__ zl) {
 #pragma unroll
   for (int qq = 0; qq < KF; ++qq) {
-    const int f = lane + 64 * qq;
+    const int f = RL::feat(qq, lane);
     if (f < Fp) {
       *reinterpret_cast<f16x8*>(zh + 8 * f) = hi[qq];
       *reinterpret_cast<f16x8*>(zl + 8 * f) = lo[qq];
@@ -296,9 +333,9 @@ __device__ __forceinline__ void write_zrow(const f16x8 (&hi)[KF], const f16x8 (&
 
 // z += p_k x_k for rows k < kn of a batch (k0 a constant after unrolling); the
 // weights of a message are broadcast as head pairs from lanes 8 k + 2 g.
-template <int KF, int NR>
-__device__ __forceinline__ void fma_rows(f32x2 (&z)[4][KF], const float (&xr)[NR][KF], float pv,
-                                         int k0, int kn) {
+template <int KF, int NR, typename RL = RowL<XF32, KF, false>>
+__device__ __forceinline__ void fma_rows(f32x2 (&z)[4][KF], const float (&xr)[NR][RL::W],
+                                         float pv, int k0, int kn) {
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     if (k == 0 || k < kn) {
@@ -306,18 +343,20 @@ __device__ __forceinline__ void fma_rows(f32x2 (&z)[4][KF], const float (&xr)[NR
 #pragma unroll
       for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * (k0 + k) + 2 * g);
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+      for (int qq = 0; qq < KF; ++qq) {
+        const float xq = RL::x(xr[k], qq);
 #pragma unroll
-        for (int qq = 0; qq < KF; ++qq)
-          z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
+        for (int g = 0; g < 4; ++g)
+          z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xq, xq}, z[g][qq]);
+      }
     }
   }
 }
 
 // z = sum over the first K rows of p_k x_k (no per-message branches: rows past
 // the slot's messages carry p = 0 on valid prefetched rows)
-template <int KF, int K, int NR>
-__device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[NR][KF], float pv) {
+template <int KF, int K, int NR, typename RL = RowL<XF32, KF, false>>
+__device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[NR][RL::W], float pv) {
   static_assert(K <= NR, "rows past the prefetched ones");
 #pragma unroll
   for (int g = 0; g < 4; ++g)
@@ -329,10 +368,12 @@ __device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[NR][K
 #pragma unroll
     for (int g = 0; g < 4; ++g) p2[g] = bcast2(pv, 8 * k + 2 * g);
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int qq = 0; qq < KF; ++qq) {
+      const float xq = RL::x(xr[k], qq);
 #pragma unroll
-      for (int qq = 0; qq < KF; ++qq)
-        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
+      for (int g = 0; g < 4; ++g)
+        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xq, xq}, z[g][qq]);
+    }
   }
 }
 
@@ -340,8 +381,8 @@ __device__ __forceinline__ void fma_k(f32x2 (&z)[4][KF], const float (&xr)[NR][K
 // h (the wave wrote its 64 lanes' p there); two broadcast 16-B reads per
 // message give the four head pairs as VGPR pairs -- 2 LDS reads instead of 8
 // v_readlane per message.
-template <int KF, int K, int NR>
-__device__ __forceinline__ void fma_k_lds(f32x2 (&z)[4][KF], const float (&xr)[NR][KF],
+template <int KF, int K, int NR, typename RL = RowL<XF32, KF, false>>
+__device__ __forceinline__ void fma_k_lds(f32x2 (&z)[4][KF], const float (&xr)[NR][RL::W],
                                           const float* __restrict__ ab) {
   static_assert(K <= NR, "rows past the prefetched ones");
 #pragma unroll
@@ -355,10 +396,12 @@ __device__ __forceinline__ void fma_k_lds(f32x2 (&z)[4][KF], const float (&xr)[N
     const f32x2 p2[4] = {f32x2{a0.x, a0.y}, f32x2{a0.z, a0.w}, f32x2{a1.x, a1.y},
                          f32x2{a1.z, a1.w}};
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int qq = 0; qq < KF; ++qq) {
+      const float xq = RL::x(xr[k], qq);
 #pragma unroll
-      for (int qq = 0; qq < KF; ++qq)
-        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xr[k][qq], xr[k][qq]}, z[g][qq]);
+      for (int g = 0; g < 4; ++g)
+        z[g][qq] = __builtin_elementwise_fma(p2[g], f32x2{xq, xq}, z[g][qq]);
+    }
     // (keeps the compiler from hoisting every read of the slot: the register
     // budget has no room for them)
     __builtin_amdgcn_sched_barrier(0);
@@ -429,11 +472,8 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
       }
     }
   };
-  float sv, xv[8][KF];
-  issue(e0, sv, xv);
-  for (int b = e0; b < e1; b += 8) {
-    float sn, xn[8][KF];
-    issue(b + 8, sn, xn);
+  // batch b: online softmax step and the 8 rows' FMAs
+  auto consume = [&](int b, float sv, const float (&xv)[8][KF]) {
     const int e = b + kk;
     const bool valid = e < e1;
     const float v = leaky(sv + t_h, slope);
@@ -465,11 +505,116 @@ __device__ __forceinline__ SegState aggregate_segment(const void* __restrict__ x
         }
       }
     }
+  };
+  float sv, xv[8][KF];
+  issue(e0, sv, xv);
+  for (int b = e0; b < e1; b += 8) {
+    float sn, xn[8][KF];
+    issue(b + 8, sn, xn);
+    consume(b, sv, xv);
     sv = sn;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
       for (int q = 0; q < KF; ++q) xv[k][q] = xn[k][q];
+  }
+  return {m, sum_xor8_16_32(l)};
+}
+
+// aggregate_segment for bf16 rows with 128 < F <= 192 whose rows start 4-B
+// aligned: lane l holds features 2 l, 2 l + 1 (one 4-B load: a bf16 pair) and
+// 128 + l (one 2-B load), so a row takes 2 VGPRs instead of 3 and NBF batches
+// of 8 rows fit in flight at 4 waves per SIMD (C5's hub chunks: half the bytes
+// of an fp32 row per message, so twice the rows in flight for the same bytes
+// per round trip).  acc[h][0 / 1] = features 2 l / 2 l + 1, acc[h][2] =
+// feature 128 + l (seg_feat).  Arithmetic identical to aggregate_segment.
+__device__ __forceinline__ int seg_feat_pair(int q, int lane) {
+  return q < 2 ? 2 * lane + q : 128 + lane;
+}
+template <int NBF>
+__device__ __forceinline__ SegState aggregate_segment_bf16p(
+    const void* __restrict__ x, int64_t ldx, int F, const int32_t* __restrict__ col, int e0,
+    int e1, const float* __restrict__ s, int lds, float t_h, float slope, float dp, uint64_t seed,
+    float (&acc)[H][3]) {
+  static_assert(NBF >= 2 && NBF <= 4, "2 .. 4 batches in flight");
+  const int lane = threadIdx.x & 63;
+  const int h = lane & 7, kk = lane >> 3;
+  const float keep_scale = dp > 0.f ? 1.0f / (1.0f - dp) : 1.0f;
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) acc[hh][q] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  int wb = e0;
+  int cw = col[min(e0 + lane, e1 - 1)];
+  int cn = col[min(e0 + 64 + lane, e1 - 1)];
+  const int f2 = 128 + lane < F ? 128 + lane : F - 1;  // clamped: never the row padding
+  const bool v2 = 128 + lane < F;
+  auto issue = [&](int b, float& sv, uint32_t (&xp)[8], uint32_t (&xs)[8]) {
+    if (b - wb == 64) {
+      wb = b;
+      cw = cn;
+      cn = col[min(b + 64 + lane, e1 - 1)];
+    }
+    const int j = __builtin_amdgcn_ds_bpermute((b - wb + kk) << 2, cw);
+    sv = lrow(s, j, lds)[h];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint16_t* xr = reinterpret_cast<const uint16_t*>(
+          xrow<XBF16>(x, __builtin_amdgcn_readlane(cw, b - wb + k), ldx));
+      xp[k] = *reinterpret_cast<const uint32_t*>(xr + 2 * lane);
+      xs[k] = xr[f2];
+    }
+  };
+  auto consume = [&](int b, float sv, const uint32_t (&xp)[8], const uint32_t (&xs)[8]) {
+    const int e = b + kk;
+    const bool valid = e < e1;
+    const float v = leaky(sv + t_h, slope);
+    const float mn = fmaxf(m, max_xor8_16_32(valid ? v : -INFINITY));
+    const float sc = __expf(m - mn);
+    float p = valid ? __expf(v - mn) : 0.f;
+    l = fmaf(l, sc, p);
+    if (b != e0 && __any(sc != 1.0f)) {
+#pragma unroll
+      for (int hh = 0; hh < H; ++hh) {
+        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), hh));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc[hh][q] *= r;
+      }
+    }
+    m = mn;
+    if (dp > 0.f) p = dropout_keep(seed, uint32_t(e), uint32_t(h), dp) ? p * keep_scale : 0.f;
+    const int nk = min(8, e1 - b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < nk) {
+        const float x0 = __uint_as_float(xp[k] << 16);
+        const float x1 = __uint_as_float(xp[k] & 0xffff0000u);
+        const float x2 = v2 ? __uint_as_float(xs[k] << 16) : 0.f;
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {
+          const float pk =
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 8 * k + hh));
+          acc[hh][0] = fmaf(pk, x0, acc[hh][0]);
+          acc[hh][1] = fmaf(pk, x1, acc[hh][1]);
+          acc[hh][2] = fmaf(pk, x2, acc[hh][2]);
+        }
+      }
+    }
+  };
+  float sv[NBF];
+  uint32_t xp[NBF][8], xs[NBF][8];
+#pragma unroll
+  for (int u = 0; u < NBF - 1; ++u) issue(e0 + 8 * u, sv[u], xp[u], xs[u]);
+  for (int b = e0; b < e1; b += 8 * NBF) {
+#pragma unroll
+    for (int u = 0; u < NBF; ++u) {
+      const int bb = b + 8 * u;
+      if (bb >= e1) break;  // wave-uniform
+      const int w = (u + NBF - 1) % NBF;
+      issue(bb + 8 * (NBF - 1), sv[w], xp[w], xs[w]);
+      consume(bb, sv[u], xp[u], xs[u]);
+    }
   }
   return {m, sum_xor8_16_32(l)};
 }

@@ -14,8 +14,16 @@ using namespace gfd::fwd;
 
 namespace {
 
-// four waves per SIMD (<= 128 VGPRs at KF = 3), two batches of 8 rows in flight each
-template <typename XT, int KF>
+// four waves per SIMD (<= 128 VGPRs at KF = 3), two batches of 8 rows in flight each;
+// PAIR (bf16 rows, 128 < F <= 192, 4-B aligned rows): GFD_HUB_NBF_PAIR batches
+// of 2-VGPR rows (aggregate_segment_bf16p)
+#ifndef GFD_HUB_PAIR
+#define GFD_HUB_PAIR 1
+#endif
+#ifndef GFD_HUB_NBF_PAIR
+#define GFD_HUB_NBF_PAIR 3  // 4: the allocator spills (1.8k VGPRs at 128)
+#endif
+template <typename XT, int KF, bool PAIR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_hub_partial(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     const float* __restrict__ s, int lds, const float* __restrict__ t, int ldt, float slope, float dp, uint64_t seed,
@@ -26,8 +34,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const int4 ck = chunks[c];
   const float t_h = lrow(t, ck.w, ldt)[lane & 7];
   float acc[H][KF];
-  SegState S =
-      aggregate_segment<XT, KF>(x, ldx, F, col, ck.y, ck.z, s, lds, t_h, slope, dp, seed, acc);
+  SegState S;
+  if constexpr (PAIR) {
+    static_assert(KF == 3, "bf16 pairs: 128 < F <= 192");
+    S = aggregate_segment_bf16p<GFD_HUB_NBF_PAIR>(x, ldx, F, col, ck.y, ck.z, s, lds, t_h, slope,
+                                                  dp, seed, acc);
+  } else {
+    S = aggregate_segment<XT, KF>(x, ldx, F, col, ck.y, ck.z, s, lds, t_h, slope, dp, seed, acc);
+  }
   const int KP = H * Fp;
   float* pr = part + c * (16 + KP);
   if (lane < 8) {
@@ -38,7 +52,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   for (int hh = 0; hh < H; ++hh)
 #pragma unroll
     for (int q = 0; q < KF; ++q) {
-      const int f = lane + 64 * q;
+      const int f = PAIR ? seg_feat_pair(q, lane) : lane + 64 * q;
       if (f < Fp) pr[16 + hh * Fp + f] = acc[hh][q];
     }
 }
@@ -112,7 +126,12 @@ template <typename XT, int KF>
 gfd_status launch_hubs_t(const AggArgs& a, const PackLayout& L, hipStream_t stream) {
   const gfd_plan& p = a.plan;
   const int64_t blocks = (p.num_chunks + 3) / 4;
-  k_hub_partial<XT, KF><<<int(blocks), 256, 0, stream>>>(
+  // bf16 pairs: 4-B loads need every row start 4-B aligned
+  const bool pair = GFD_HUB_PAIR && XT::kBytes == 2 && KF == 3 && a.F > 128 &&
+                    reinterpret_cast<uintptr_t>(a.x) % 4 == 0 && a.ldx % 2 == 0;
+  auto kern = pair ? &k_hub_partial<XT, KF, (XT::kBytes == 2 && KF == 3)>
+                   : &k_hub_partial<XT, KF, false>;
+  kern<<<int(blocks), 256, 0, stream>>>(
       a.x, a.F, L.Fp, a.ldx, a.col, a.s, a.lds, a.t, a.ldt, a.slope, a.dp, a.seed,
       reinterpret_cast<const int4*>(p.hub_chunk), p.num_chunks, a.part);
   GFD_LAUNCH_CHECK();

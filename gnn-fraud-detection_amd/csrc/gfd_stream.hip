@@ -92,6 +92,13 @@ constexpr int kSWaves = 8;
 #ifndef GFD_LIGHT_LO_AP_BF16
 #define GFD_LIGHT_LO_AP_BF16 2
 #endif
+#ifndef GFD_LIGHT_LO_WL
+#define GFD_LIGHT_LO_WL 8
+#endif
+// bf16 rows held as RowL pairs (2 VGPRs a row instead of 3) where they allow it
+#ifndef GFD_STREAM_PAIRS
+#define GFD_STREAM_PAIRS 1
+#endif
 // A-fragment k-steps read ahead in the MFMA loop (general; light fp32 / bf16
 // rows).  Light fp32: 1 keeps the kernel spill-free with 6 rows per slot in
 // flight (C4 light 6.73 -> 6.22 ms against 2); light bf16: 2 (C5 33.3 vs 33.7 ms)
@@ -103,29 +110,36 @@ constexpr int ap_of() {
        : LIGHT ? (XT::kBytes == 2 ? GFD_LIGHT_AP_BF16 : GFD_LIGHT_AP) : GFD_GENERAL_AP;
 }
 // x rows of a general slot issued one tile ahead (the rest of batch 0 is
-// issued when its aggregation starts).  fp32 rows: none -- the kernel is then
-// spill-free and C4's general stage 3.13 -> 3.00 ms; bf16 rows: 4 (without them
-// C5's general stage 35.8 -> 56.2 ms: the half-size rows issued during the MFMA
-// phase hide most of a round trip)
+// issued when its aggregation starts).  fp32 rows: 4 since round 6 (the two
+// slots sharing their batch registers left room: spill-free at 255 VGPRs;
+// C4 general -0.04..-0.07 ms, profiles/r6q_hub_pairs_general_nl4_ab.txt --
+// until then 0: 3.13 -> 3.00 ms against the spilling 4 of round 2); bf16 rows:
+// 4 (without them C5's general stage 35.8 -> 56.2 ms: the half-size rows
+// issued during the MFMA phase hide most of a round trip)
 #ifndef GFD_GENERAL_NL_F32
-#define GFD_GENERAL_NL_F32 0
+#define GFD_GENERAL_NL_F32 4
 #endif
 #ifndef GFD_GENERAL_NL_BF16
 #define GFD_GENERAL_NL_BF16 4
 #endif
-template <int LIGHT, typename XT>
+// ... bf16 rows held as RowL pairs (2 VGPRs a row)
+#ifndef GFD_GENERAL_NL_BF16P
+#define GFD_GENERAL_NL_BF16P 4
+#endif
+template <int LIGHT, typename XT, bool PR = false>
 constexpr int nl_of() {
   return LIGHT == 2 ? kLightLo
-       : LIGHT ? kLightMax : (XT::kBytes == 2 ? GFD_GENERAL_NL_BF16 : GFD_GENERAL_NL_F32);
+       : LIGHT ? kLightMax
+       : (XT::kBytes == 2 ? (PR ? GFD_GENERAL_NL_BF16P : GFD_GENERAL_NL_BF16) : GFD_GENERAL_NL_F32);
 }
 
 #ifdef GFD_PROF
 // Diagnostic build only (GFD_BUILD_VARIANT=prof GFD_EXTRA_FLAGS=-DGFD_PROF):
 // per-wave s_memtime cycles of the tile loop phases, summed over waves,
-// [light][phase]: 0 MFMA + next-tile issue, 1 barrier 1, 2 aggregation,
+// [LIGHT: 0 general, 1 light, 2 short light][phase]: 0 MFMA + next-tile issue, 1 barrier 1, 2 aggregation,
 // 3 barrier 2; [light][4] tiles; [light][5] cycles from the loop top to the
 // end of k-step 0 (the first issue piece: waits for the slot records).  Read by gfd_prof_read (scripts/prof_phases.py).
-__device__ unsigned long long g_prof[2][6];
+__device__ unsigned long long g_prof[3][6];
 #endif
 
 struct SlotRec {  // one tile slot as loaded (vector loads: no SMEM in the lgkm queue)
@@ -139,13 +153,13 @@ struct SlotRing {  // a slot record parked in LDS between issue and aggregation
   int j[8];        // sources of messages 0..7 (general slots)
 };
 
-template <int KF, int NRW = 4>
+template <int KF, int NRW = 4, int W = KF>
 struct SlotRows {  // a slot's first (and, for light slots, only) batch in flight
   float th;        // t_i of head lane & 7
   float sj;        // s_j of the lane's message (lane >> 3)
   int cj;          // general: source of message 8 + lane (0 past the end)
   int n;           // messages of the slot (wave-uniform; set with the logits)
-  float xv[NRW][KF];  // x rows of messages 0 .. NRW - 1 (lane <-> feature)
+  float xv[NRW][W];  // x rows of messages 0 .. NRW - 1 (RowL layout, W registers a row)
 };
 
 // live: slot < lim (<= num_dst): the light launch stops at the first lone slot
@@ -164,8 +178,8 @@ __device__ __forceinline__ void sl_rec(SlotRec& p, int64_t slot, int64_t num_dst
 // window (general) and the ring record; part 1 + k = x row k.  Issued
 // unconditionally (past the last slot: clamped, ignored records), so no
 // branch joins in-flight loads.
-template <int PART, typename XT, int KF, int LIGHT, int NRW>
-__device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW>& q,
+template <int PART, typename XT, int KF, int LIGHT, typename RL, int NRW>
+__device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW, RL::W>& q,
                                               const void* __restrict__ x, int64_t ldx, int F,
                                               const int32_t* __restrict__ col,
                                               const float* __restrict__ s, int lds,
@@ -196,33 +210,33 @@ __device__ __forceinline__ void sl_issue_part(const SlotRec& p, SlotRows<KF, NRW
     // padding sources repeat the last one) fetch nothing and read zeros
     constexpr int k = PART - 1;
     const int jk = __builtin_amdgcn_readlane(p.v, 8 + k);
-    row_regs<XT, KF>(xrow<XT>(x, jk, ldx), F, lane, k < q.n, q.xv[k]);
+    RL::load(xrow<XT>(x, jk, ldx), F, lane, k < q.n, q.xv[k]);
   }
 }
 
 // z = sum of the first kmax (2 .. NR, wave-uniform) rows, one straight-line
 // block per count (K = 2 .. NR)
-template <int KF, int NR, int K = 2>
-__device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[NR][KF], float p,
-                                          int kmax) {
+template <int KF, int NR, typename RL, int K = 2>
+__device__ __forceinline__ void light_fma(f32x2 (&z)[4][KF], const float (&xv)[NR][RL::W],
+                                          float p, int kmax) {
   static_assert(NR >= 2 && NR <= 7, "light slots: 2 .. 7 messages");
   if constexpr (K >= NR) {
-    fma_k<KF, NR>(z, xv, p);
+    fma_k<KF, NR, NR, RL>(z, xv, p);
   } else {
-    if (kmax <= K) fma_k<KF, K>(z, xv, p);
-    else light_fma<KF, NR, K + 1>(z, xv, p, kmax);
+    if (kmax <= K) fma_k<KF, K, NR, RL>(z, xv, p);
+    else light_fma<KF, NR, RL, K + 1>(z, xv, p, kmax);
   }
 }
 
 // light_fma with the weights from the wave's LDS buffer (fma_k_lds)
-template <int KF, int NR, int K = 2>
-__device__ __forceinline__ void light_fma_lds(f32x2 (&z)[4][KF], const float (&xv)[NR][KF],
+template <int KF, int NR, typename RL, int K = 2>
+__device__ __forceinline__ void light_fma_lds(f32x2 (&z)[4][KF], const float (&xv)[NR][RL::W],
                                               const float* __restrict__ ab, int kmax) {
   if constexpr (K >= NR) {
-    fma_k_lds<KF, NR>(z, xv, ab);
+    fma_k_lds<KF, NR, NR, RL>(z, xv, ab);
   } else {
-    if (kmax <= K) fma_k_lds<KF, K>(z, xv, ab);
-    else light_fma_lds<KF, NR, K + 1>(z, xv, ab, kmax);
+    if (kmax <= K) fma_k_lds<KF, K, NR, RL>(z, xv, ab);
+    else light_fma_lds<KF, NR, RL, K + 1>(z, xv, ab, kmax);
   }
 }
 
@@ -231,8 +245,8 @@ __device__ __forceinline__ void light_fma_lds(f32x2 (&z)[4][KF], const float (&x
 // one, so the head-mean shortcut of k_lone does not apply): straight-line
 // code, the softmax sum and reciprocal independent of the FMA block.  kmax:
 // messages to run (wave-uniform, >= n).
-template <int KF, int NR>
-__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, NR>& q, int kmax,
+template <int KF, typename RL, int NR>
+__device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, NR, RL::W>& q, int kmax,
                                          float slope, float dp, uint64_t seed, int Fp,
                                          float* __restrict__ stats,
                                          _Float16* __restrict__ zh, _Float16* __restrict__ zl,
@@ -270,21 +284,21 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, NR>& q
     const float ps = pd * (inv * ldexpf(1.0f, erg));
 #if GFD_LIGHT_ALDS
     ab[lane] = ps;  // this wave's own buffer: its LDS operations run in order
-    light_fma_lds<KF, NR>(z, q.xv, ab, kmax);
+    light_fma_lds<KF, NR, RL>(z, q.xv, ab, kmax);
 #else
-    light_fma<KF, NR>(z, q.xv, ps, kmax);
+    light_fma<KF, NR, RL>(z, q.xv, ps, kmax);
 #endif
     split_zrow<KF>(z, hi, lo);
   } else {
 #if GFD_LIGHT_ALDS
     ab[lane] = pd;
-    light_fma_lds<KF, NR>(z, q.xv, ab, kmax);
+    light_fma_lds<KF, NR, RL>(z, q.xv, ab, kmax);
 #else
-    light_fma<KF, NR>(z, q.xv, pd, kmax);
+    light_fma<KF, NR, RL>(z, q.xv, pd, kmax);
 #endif
     er = pack_zrow<KF>(z, inv, erg, hi, lo);
   }
-  write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
+  write_zrow<KF, RL>(hi, lo, Fp, lane, zh, zl);
   if (lane == 0) {
     rsc[r] = ldexpf(1.0f, -er);
     rid[r] = d.x;
@@ -304,9 +318,10 @@ __device__ __forceinline__ void sl_light(const int4 d, const SlotRows<KF, NR>& q
 //  * xa / xb (8 rows of a batch) belong to the caller: the wave's two slots
 //    share them, which keeps the bf16 instance (4 rows a tile ahead) spill-free
 //    (C5 general stage 34.4 -> 25.9 ms; profiles/r6p_general_rows_ab.txt).
-template <typename XT, int KF, int NRW, int NRA>
+template <typename XT, int KF, typename RL, int NRW, int NRA>
 __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
-                                           const SlotRows<KF, NRA>& q, const void* __restrict__ x,
+                                           const SlotRows<KF, NRA, RL::W>& q,
+                                           const void* __restrict__ x,
                                            int64_t ldx, int F, int Fp,
                                            const int32_t* __restrict__ col,
                                            const float* __restrict__ s, int lds, float slope, float dp,
@@ -314,7 +329,7 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
                                            float* __restrict__ stats, _Float16* __restrict__ zh,
                                            _Float16* __restrict__ zl, float* __restrict__ rsc,
                                            int* __restrict__ rid, int r, int erg, int lane,
-                                           float (&xa)[4][KF], float (&xb)[4][KF]) {
+                                           float (&xa)[4][RL::W], float (&xb)[4][RL::W]) {
   const int4 d = uni4(ring->d);
   const int j0 = ring->j[lane >> 3];
   const int h = lane & 7, kk = lane >> 3;
@@ -322,13 +337,12 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
   auto issue0 = [&](int ja, int na) {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(ja, 8 * k), ldx), F, lane, k < na,
-                       xa[k]);
+      RL::load(xrow<XT>(x, __builtin_amdgcn_readlane(ja, 8 * k), ldx), F, lane, k < na, xa[k]);
     if (na > 4) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(ja, 8 * (4 + k)), ldx), F, lane,
-                         4 + k < na, xb[k]);
+        RL::load(xrow<XT>(x, __builtin_amdgcn_readlane(ja, 8 * (4 + k)), ldx), F, lane,
+                 4 + k < na, xb[k]);
     }
   };
   f32x2 z[4][KF];
@@ -347,7 +361,7 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
     for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int qq = 0; qq < KF; ++qq) {
-        const int f = lane + 64 * qq;
+        const int f = RL::feat(qq, lane);
         if (f < Fp) z[g][qq] = f32x2{src[2 * g * Fp + f], src[(2 * g + 1) * Fp + f]};
       }
   } else {
@@ -364,17 +378,20 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
       l = pv;
       if (dp > 0.f) pv = dropout_keep(seed, uint32_t(e0 + kk), uint32_t(h), dp) ? pv * keep : 0.f;
       if constexpr (NRW == 0) {
-        fma_rows<KF, 4>(z, xa, pv, 0, min(4, n));
-        if (n > 4) fma_rows<KF, 4>(z, xb, pv, 4, min(4, n - 4));
+        fma_rows<KF, 4, RL>(z, xa, pv, 0, min(4, n));
+        if (n > 4) fma_rows<KF, 4, RL>(z, xb, pv, 4, min(4, n - 4));
+      } else if constexpr (NRW == 8) {  // the whole batch issued a tile ahead
+        fma_rows<KF, 8, RL>(z, q.xv, pv, 0, min(8, n));
       } else {
-        fma_rows<KF, 4>(z, q.xv, pv, 0, min(4, n));
+        static_assert(NRW == 4, "general slots: 0, 4 or 8 rows a tile ahead");
+        fma_rows<KF, 4, RL>(z, q.xv, pv, 0, min(4, n));
       }
-      if (NRW > 0 && n > 4) {  // rows 4..7
+      if (NRW == 4 && n > 4) {  // rows 4..7
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), ldx), F, lane,
-                           4 + k < n, xb[k]);
-        fma_rows<KF, 4>(z, xb, pv, 4, min(4, n - 4));
+          RL::load(xrow<XT>(x, __builtin_amdgcn_readlane(j0, 8 * (4 + k)), ldx), F, lane,
+                   4 + k < n, xb[k]);
+        fma_rows<KF, 4, RL>(z, xb, pv, 4, min(4, n - 4));
       }
     }
     // batches 1..: loads of batch b issued at the end of batch b - 8
@@ -391,13 +408,13 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
       sv = lrow(s, jl, lds)[h];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(cj, b - cb + k), ldx), F, lane,
-                         b + k < n, xa[k]);
+        RL::load(xrow<XT>(x, __builtin_amdgcn_readlane(cj, b - cb + k), ldx), F, lane,
+                 b + k < n, xa[k]);
       if (n - b > 4) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          row_regs<XT, KF>(xrow<XT>(x, __builtin_amdgcn_readlane(cj, b - cb + 4 + k), ldx), F,
-                           lane, b + 4 + k < n, xb[k]);
+          RL::load(xrow<XT>(x, __builtin_amdgcn_readlane(cj, b - cb + 4 + k), ldx), F,
+                   lane, b + 4 + k < n, xb[k]);
       }
     };
     if (n > 8) issue(8);
@@ -420,8 +437,8 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
       m = mn;
       if (dp > 0.f)
         pv = dropout_keep(seed, uint32_t(e0 + b + kk), uint32_t(h), dp) ? pv * keep : 0.f;
-      fma_rows<KF, 4>(z, xa, pv, 0, min(4, n - b));
-      if (n - b > 4) fma_rows<KF, 4>(z, xb, pv, 4, min(4, n - b - 4));
+      fma_rows<KF, 4, RL>(z, xa, pv, 0, min(4, n - b));
+      if (n - b > 4) fma_rows<KF, 4, RL>(z, xb, pv, 4, min(4, n - b - 4));
       if (b + 8 < n) issue(b + 8);
     }
     l = sum_xor8_16_32(l);
@@ -434,14 +451,15 @@ __device__ __forceinline__ void sl_general(const SlotRing* __restrict__ ring,
   }
   f16x8 hi[KF], lo[KF];
   const int er = pack_zrow<KF>(z, inv, erg, hi, lo);
-  write_zrow<KF>(hi, lo, Fp, lane, zh, zl);
+  write_zrow<KF, RL>(hi, lo, Fp, lane, zh, zl);
   if (lane == 0) {
     rsc[r] = ldexpf(1.0f, -er);
     rid[r] = d.x;
   }
 }
 
-template <typename XT, int KF, int KHM, int LO, bool EXACT, int LIGHT, bool EPI>
+// PR: bf16 rows held as RowL pairs (2 VGPRs a row; 128 < F <= 192, 4-B aligned rows)
+template <typename XT, int KF, int KHM, int LO, bool EXACT, int LIGHT, bool EPI, bool PR>
 __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     const void* __restrict__ x, int F, int Fp, int64_t ldx, const int32_t* __restrict__ col,
     int64_t num_dst, const int4* __restrict__ desc,
@@ -517,24 +535,25 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #endif
 
   SlotRec n0, n1;
-  constexpr int NL = nl_of<LIGHT, XT>();  // rows issued one tile ahead per slot
+  constexpr int NL = nl_of<LIGHT, XT, PR>();  // rows issued one tile ahead per slot
   constexpr int NA = NL > 0 ? NL : 1;      // (register arrays of at least one row)
-  SlotRows<KF, NA> d0, d1;
+  using RL = RowL<XT, KF, PR>;
+  SlotRows<KF, NA, RL::W> d0, d1;
   // prologue: tile 0 issued and aggregated; records of tile 1 loading
   sl_rec(n0, slot(0, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(0, r1), num_dst, lim, desc, cols8, lane);
 #define GFD_ISSUE(P, n, d, ring) \
-  sl_issue_part<P, XT, KF, LIGHT>(n, d, x, ldx, F, col, s, lds, t, ldt, ring, lane)
+  sl_issue_part<P, XT, KF, LIGHT, RL>(n, d, x, ldx, F, col, s, lds, t, ldt, ring, lane)
 #define GFD_ROW(k, n, d, ring) \
   if constexpr (NL >= k) GFD_ISSUE((NL >= k ? k : 0), n, d, ring)
   GFD_ISSUE(0, n0, d0, ring0 + r0);
   GFD_ROW(1, n0, d0, ring0 + r0); GFD_ROW(2, n0, d0, ring0 + r0); GFD_ROW(3, n0, d0, ring0 + r0);
   GFD_ROW(4, n0, d0, ring0 + r0); GFD_ROW(5, n0, d0, ring0 + r0); GFD_ROW(6, n0, d0, ring0 + r0);
-  GFD_ROW(7, n0, d0, ring0 + r0);
+  GFD_ROW(7, n0, d0, ring0 + r0); GFD_ROW(8, n0, d0, ring0 + r0);
   GFD_ISSUE(0, n1, d1, ring0 + r1);
   GFD_ROW(1, n1, d1, ring0 + r1); GFD_ROW(2, n1, d1, ring0 + r1); GFD_ROW(3, n1, d1, ring0 + r1);
   GFD_ROW(4, n1, d1, ring0 + r1); GFD_ROW(5, n1, d1, ring0 + r1); GFD_ROW(6, n1, d1, ring0 + r1);
-  GFD_ROW(7, n1, d1, ring0 + r1);
+  GFD_ROW(7, n1, d1, ring0 + r1); GFD_ROW(8, n1, d1, ring0 + r1);
   sl_rec(n0, slot(1, r0), num_dst, lim, desc, cols8, lane);
   sl_rec(n1, slot(1, r1), num_dst, lim, desc, cols8, lane);
   auto aggregate = [&](int tpar) {  // this wave's two slots of the tile in parity tpar
@@ -548,15 +567,15 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       // parity, free between barrier 1 and the next MFMA phase (its last
       // reader, reduce_store of tile v - 1, ran before barrier 1); 2 x 256 B per wave
       float* ab = reinterpret_cast<float*>(red0 + tpar * 4 * 64) + wave * 128;
-      sl_light<KF>(da, d0, kmax, slope, dp, seed, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid,
+      sl_light<KF, RL>(da, d0, kmax, slope, dp, seed, Fp, stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid,
                    r0, erg, ab, lane);
-      sl_light<KF>(db, d1, kmax, slope, dp, seed, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid,
+      sl_light<KF, RL>(db, d1, kmax, slope, dp, seed, Fp, stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid,
                    r1, erg, ab + 64, lane);
     } else {
-      float xa[4][KF], xb[4][KF];  // the two slots' batch registers (sl_general)
-      sl_general<XT, KF, NL, NA>(rg + r0, d0, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
+      float xa[4][RL::W], xb[4][RL::W];  // the two slots' batch registers (sl_general)
+      sl_general<XT, KF, RL, NL, NA>(rg + r0, d0, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
                                  stats, Zh + r0 * ZS, Zl + r0 * ZS, rsc, rid, r0, erg, lane, xa, xb);
-      sl_general<XT, KF, NL, NA>(rg + r1, d1, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
+      sl_general<XT, KF, RL, NL, NA>(rg + r1, d1, x, ldx, F, Fp, col, s, lds, slope, dp, seed, zhub,
                                  stats, Zh + r1 * ZS, Zl + r1 * ZS, rsc, rid, r1, erg, lane, xa, xb);
     }
   };
@@ -648,13 +667,13 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       GFD_PROW(1, 1, n0, d0, rg + r0); GFD_PROW(2, 2, n0, d0, rg + r0);
       GFD_PROW(3, 3, n0, d0, rg + r0); GFD_PROW(4, 4, n0, d0, rg + r0);
       GFD_PROW(5, 5, n0, d0, rg + r0); GFD_PROW(6, 6, n0, d0, rg + r0);
-      GFD_PROW(7, 7, n0, d0, rg + r0);
+      GFD_PROW(7, 7, n0, d0, rg + r0); GFD_PROW(8, 8, n0, d0, rg + r0);
       if (GFD_PIECE(NL)) sl_rec(n0, slot(v + 2, r0), num_dst, lim, desc, cols8, lane);
       if (GFD_PIECE(NL + 1)) GFD_ISSUE(0, n1, d1, rg + r1);
       GFD_PROW(NL + 2, 1, n1, d1, rg + r1); GFD_PROW(NL + 3, 2, n1, d1, rg + r1);
       GFD_PROW(NL + 4, 3, n1, d1, rg + r1); GFD_PROW(NL + 5, 4, n1, d1, rg + r1);
       GFD_PROW(NL + 6, 5, n1, d1, rg + r1); GFD_PROW(NL + 7, 6, n1, d1, rg + r1);
-      GFD_PROW(NL + 8, 7, n1, d1, rg + r1);
+      GFD_PROW(NL + 8, 7, n1, d1, rg + r1); GFD_PROW(NL + 9, 8, n1, d1, rg + r1);
 #undef GFD_PROW
       if (GFD_PIECE(2 * NL + 1)) sl_rec(n1, slot(v + 2, r1), num_dst, lim, desc, cols8, lane);
 #undef GFD_PIECE
@@ -711,9 +730,9 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
 #ifdef GFD_PROF
   if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) atomicAdd(&g_prof[LIGHT ? 1 : 0][i], pc[i]);
-    if (wave == 0) atomicAdd(&g_prof[LIGHT ? 1 : 0][4], (unsigned long long)nv);
-    atomicAdd(&g_prof[LIGHT ? 1 : 0][5], pc[4]);
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_prof[LIGHT][i], pc[i]);
+    if (wave == 0) atomicAdd(&g_prof[LIGHT][4], (unsigned long long)nv);
+    atomicAdd(&g_prof[LIGHT][5], pc[4]);
   }
 #endif
 #undef GFD_ROW
@@ -732,12 +751,12 @@ size_t stream_smem(int Fp, int lo) {
          sizeof(int) * 2 * kTile;
 }
 
-template <typename XT, int KF, int KHM, int LO, bool EXACT, int LIGHT>
+template <typename XT, int KF, int KHM, int LO, bool EXACT, int LIGHT, bool PR = false>
 gfd_status launch_stream_k(const AggArgs& a, const PackLayout& L, bool to_end,
                            hipStream_t stream) {
   const bool epi = a.ep.ab != nullptr || a.ep.hout != nullptr;
-  auto kern = epi ? &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, true>
-                  : &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, false>;
+  auto kern = epi ? &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, true, PR>
+                  : &k_stream<XT, KF, KHM, LO, EXACT, LIGHT, false, PR>;
   if (EXACT && L.KS / 2 != KHM) return GFD_ERR_UNSUPPORTED;
   const size_t lds = stream_smem(L.Fp, LO);
   if (L.KS / 2 > KHM || lds > kLdsBytes) return GFD_ERR_UNSUPPORTED;
@@ -772,8 +791,21 @@ gfd_status launch_stream_x(const AggArgs& a, const PackLayout& L, bool to_end,
                          : launch_stream_k<XT, 1, 8, 0, false, LIGHT>(a, L, to_end, stream);
     case 2: return exact ? launch_stream_k<XT, 2, 16, 0, true, LIGHT>(a, L, to_end, stream)
                          : launch_stream_k<XT, 2, 16, 0, false, LIGHT>(a, L, to_end, stream);
-    case 3: return exact ? launch_stream_k<XT, 3, 21, 8, true, LIGHT>(a, L, to_end, stream)
-                         : launch_stream_k<XT, 3, 21, 8, false, LIGHT>(a, L, to_end, stream);
+    case 3: {
+      // W_lo k-steps in LDS: 8 (the registers go to rows in flight); the short
+      // light tiles have registers to spare, but 4 (GFD_LIGHT_LO_WL) measured
+      // the same (profiles/r6q_hub_pairs_general_nl4_ab.txt)
+      constexpr int LO = LIGHT == 2 ? GFD_LIGHT_LO_WL : 8;
+      // bf16 rows with F > 128 and 4-B aligned row starts: RowL pairs
+      constexpr bool kB = XT::kBytes == 2;
+      const bool pr = GFD_STREAM_PAIRS && kB && a.F > 128 &&
+                      reinterpret_cast<uintptr_t>(a.x) % 4 == 0 && a.ldx % 2 == 0;
+      if (pr)
+        return exact ? launch_stream_k<XT, 3, 21, LO, true, LIGHT, kB>(a, L, to_end, stream)
+                     : launch_stream_k<XT, 3, 21, LO, false, LIGHT, kB>(a, L, to_end, stream);
+      return exact ? launch_stream_k<XT, 3, 21, LO, true, LIGHT>(a, L, to_end, stream)
+                   : launch_stream_k<XT, 3, 21, LO, false, LIGHT>(a, L, to_end, stream);
+    }
     default: return GFD_ERR_UNSUPPORTED;
   }
 }
@@ -808,10 +840,10 @@ gfd_status launch_light(const AggArgs& a, const PackLayout& L, bool to_end,
 }  // namespace gfd
 
 #ifdef GFD_PROF
-extern "C" int gfd_prof_read(unsigned long long* out12, int reset) {
-  if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_prof), sizeof(g_prof)) != hipSuccess) return 1;
+extern "C" int gfd_prof_read(unsigned long long* out18, int reset) {
+  if (hipMemcpyFromSymbol(out18, HIP_SYMBOL(g_prof), sizeof(g_prof)) != hipSuccess) return 1;
   if (reset) {
-    static const unsigned long long zero[2][6] = {};
+    static const unsigned long long zero[3][6] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), zero, sizeof(zero)) != hipSuccess) return 1;
   }
   return 0;

@@ -34,9 +34,10 @@ def per_kernel(d):
 
 def stage_of(k):
     if k.startswith("k_stream<"):
-        # k_stream<XT, KF, KHM, LO, EXACT, LIGHT, EPI>
+        # k_stream<XT, KF, KHM, LO, EXACT, LIGHT, EPI>; LIGHT 0 general, 1 light,
+        # 2 short light (round 6; "true" / "false" before)
         args = [a.strip() for a in k[k.index("<") + 1:k.rindex(">")].split(",")]
-        return "light" if args[5] == "true" else "general"
+        return "light" if args[5] in ("true", "1", "2") else "general"
     if k.startswith(("k_hub_partial", "k_hub_fin")):
         return "hubs"
     if k.startswith(("k_logits_lone", "k_wmax", "k_pack_")):

@@ -26,7 +26,7 @@ def main():
     lib = _lib.load()
     rd = lib.gfd_prof_read
     rd.argtypes = [ct.c_void_p, ct.c_int]
-    buf = (ct.c_ulonglong * 12)()
+    buf = (ct.c_ulonglong * 18)()
     for _ in range(2):
         layer.step()
     torch.cuda.synchronize()
@@ -37,7 +37,7 @@ def main():
     torch.cuda.synchronize()
     rd(buf, 0)
     names = ("MFMA + next-tile issue", "barrier 1", "aggregation", "barrier 2")
-    for cls, k in (("general", 0), ("light", 1)):
+    for cls, k in (("general", 0), ("light", 1), ("short light", 2)):
         v = [buf[6 * k + i] for i in range(6)]
         tot = sum(v[:4])
         tiles = v[4] / steps
