@@ -137,8 +137,9 @@ constexpr int nl_of() {
 // Diagnostic build only (GFD_BUILD_VARIANT=prof GFD_EXTRA_FLAGS=-DGFD_PROF):
 // per-wave s_memtime cycles of the tile loop phases, summed over waves,
 // [LIGHT: 0 general, 1 light, 2 short light][phase]: 0 MFMA + next-tile issue, 1 barrier 1, 2 aggregation,
-// 3 barrier 2; [light][4] tiles; [light][5] cycles from the loop top to the
-// end of k-step 0 (the first issue piece: waits for the slot records).  Read by gfd_prof_read (scripts/prof_phases.py).
+// 3 barrier 2; [light][4] tiles; [light][5] cycles of the aggregation spent
+// waiting for the loads in flight at its start (an explicit vmcnt(0) wait).
+// Read by gfd_prof_read (scripts/prof_phases.py).
 __device__ unsigned long long g_prof[3][6];
 #endif
 
@@ -678,9 +679,6 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
       if (GFD_PIECE(2 * NL + 1)) sl_rec(n1, slot(v + 2, r1), num_dst, lim, desc, cols8, lane);
 #undef GFD_PIECE
       if (u == KHM - 2 && !kh && v > 0) reduce_store(acc_prev, pn);  // tile v - 1
-#ifdef GFD_PROF
-      if (u == 1) pc[4] += __builtin_amdgcn_s_memtime() - ts0;
-#endif
       if (u < KH) {
         const f16x8 ahi = phi[u % kAP], alo = plo[u % kAP];
         f16x8 blo = u < NR ? bl[u < NR ? u : 0] : pwl[u % kAP];
@@ -710,6 +708,11 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
     __syncthreads();  // partials visible; every Z read of this tile done
 #ifdef GFD_PROF
     const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+    // the wait for every load in flight (the next tile's rows, issued during
+    // the MFMA phase) before the aggregation: [5] (this stamp's own wait moves
+    // the aggregation's first waits here)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pc[4] += __builtin_amdgcn_s_memtime() - ts2;
 #endif
 
     // ---- tile v + 1: aggregate its rows into Z ----

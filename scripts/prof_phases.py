@@ -46,7 +46,7 @@ def main():
               f"{tot / steps / max(tiles, 1) / waves_per_tile:.0f} cycles per tile (per wave)")
         for n, x in zip(names, v[:4]):
             print(f"   {n:24s} {100.0 * x / max(tot, 1):5.1f} %")
-        print(f"   {'(of MFMA: to k-step 1)':24s} {100.0 * v[5] / max(tot, 1):5.1f} %")
+        print(f"   {'(of aggregation: rows)':24s} {100.0 * v[5] / max(tot, 1):5.1f} %")
 
 
 if __name__ == "__main__":
