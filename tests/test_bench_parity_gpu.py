@@ -321,21 +321,26 @@ def test_heavy_tailed_features_sharded(big):
     assert_close(torch.cat(parts), _oracle(x, ei, W, a_s, a_d, b), what=f"sharded outlier {big:g}")
 
 
-@pytest.mark.parametrize("F", [100, 166])
-def test_nan_row_padding_and_last_row_at_allocation_end(F):
+@pytest.mark.parametrize("dtype,F,ldx", [(torch.float32, 100, 112), (torch.float32, 166, 176),
+                                         (torch.bfloat16, 166, 192), (torch.bfloat16, 100, 128),
+                                         (torch.bfloat16, 166, 176)])
+def test_nan_row_padding_and_last_row_at_allocation_end(dtype, F, ldx):
     """x with row pitch > F whose padding columns hold NaN, and whose last row
     ends exactly at the end of the allocation: lanes f >= F must read zeros
-    (buffer range check), never the padding or past the allocation."""
+    (buffer range check), never the padding or past the allocation.  Pitches
+    that cover the logits pass's padded last k-step (fp32 16 * ceil(F / 16),
+    bf16 32 * ceil(F / 32)) take its whole-vector tail loads (padding zeroed in
+    registers) on every tile but the last; 166 / 176 bf16 does not."""
     N = 5000
     ei, x, W, a_s, a_d, b = _small(N, 40000, F, seed=14)
-    ldx = (F + 7) // 8 * 8 + 8
-    buf = torch.full((N * ldx - (ldx - F),), float("nan"), device=DEV)
+    x = x.to(dtype)
+    buf = torch.full((N * ldx - (ldx - F),), float("nan"), device=DEV, dtype=dtype)
     xv = buf.as_strided((N, F), (ldx, 1))
     xv.copy_(x.to(DEV))
     assert torch.isnan(buf.as_strided((N - 1, ldx - F), (ldx, 1), F)).all()
     out = _gfd(xv, ei, W, a_s, a_d, b)
     assert torch.isfinite(out).all()
-    assert_close(out, _oracle(x, ei, W, a_s, a_d, b), what=f"NaN padding F={F}")
+    assert_close(out, _oracle(x.float(), ei, W, a_s, a_d, b), what=f"NaN padding {dtype} F={F} ldx={ldx}")
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
