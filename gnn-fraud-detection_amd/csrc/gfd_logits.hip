@@ -61,7 +61,7 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <typename XT, int KS, bool HEAD, bool A16, bool EPI, bool WIDE>
+template <typename XT, int KS, bool HEAD, bool A16, bool EPI>
 __global__ void __launch_bounds__(kLLWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_logits_lone(
     const typename XT::T* __restrict__ x, int64_t rows, int F, int64_t ldx,
@@ -71,7 +71,7 @@ k_logits_lone(
     const int32_t* __restrict__ rowptr, const float* __restrict__ bias, float slope,
     float* __restrict__ sl, int lds, float* __restrict__ tl, int ldt, float* __restrict__ xmax,
     float* __restrict__ out,
-    float* __restrict__ stats, Epi ep, int64_t t_begin, int64_t t_end) {
+    float* __restrict__ stats, Epi ep) {
   extern __shared__ __attribute__((aligned(16))) char lsm[];
   // permuted Wbar hi / lo fragments [2][kLKB][4][64], zero past KB
   uint4 (*WB)[kLKB][4][64] = reinterpret_cast<uint4 (*)[kLKB][4][64]>(lsm);
@@ -112,16 +112,11 @@ k_logits_lone(
   float am = 0.f;  // max |x| over the values this lane loaded
   const int64_t wave = int64_t(blockIdx.x) * kLLWaves + (threadIdx.x >> 6);
   const int64_t nwave = int64_t(gridDim.x) * kLLWaves;
-  for (int64_t t = t_begin + wave; t < t_end; t += nwave) {
+  const int64_t tiles = (rows + 15) / 16;
+  for (int64_t t = wave; t < tiles; t += nwave) {
     int lane = lane0, rl = lane & 15, g = lane >> 4;
     const int64_t row = t * 16 + rl;
     const bool rin = row < rows;
-    // WIDE: the ragged last k-step as ONE vector load per lane (the features
-    // past F zeroed in registers); the host launches it where the row pitch
-    // covers the whole k-step, over tiles without the array's last row, whose
-    // pitch is allocated (the next row follows).  Otherwise up to 8 scalar
-    // loads a lane (the last tile: its own launch)
-    constexpr bool wide = WIDE;
     // fp32: lane group g holds features 16 s + 4 g .. +3 of fp32 k-step s (the
     // permuted fragment order); bf16: features 32 t + 8 g .. +7 of f16 k-step
     // t in one 16-B load (the plain order)
@@ -135,7 +130,7 @@ k_logits_lone(
 #pragma unroll
       for (int tt = 0; tt < kLKB; ++tt) {
         const int f0 = 32 * tt + 8 * g;
-        if (tt < KB && (f0 + 8 <= F || (wide && tt == KB - 1))) {
+        if (tt < KB && f0 + 8 <= F) {
           if constexpr (A16) {
             hb[tt] = *reinterpret_cast<const uint4*>(xh + 32 * tt);
           } else {  // 8-B aligned rows (a row pitch of 4 k bf16): two 8-B loads
@@ -143,16 +138,7 @@ k_logits_lone(
             const uint2 u1 = *reinterpret_cast<const uint2*>(xh + 32 * tt + 4);
             hb[tt] = make_uint4(u0.x, u0.y, u1.x, u1.y);
           }
-          if (tt == KB - 1) {  // the ragged k-step read whole: features >= F -> 0
-            // (valid count from an opaque lane id: per tile, not hoisted into VGPRs)
-            const int nv = F - (32 * tt + 8 * (opaque(lane0) >> 4));
-            uint32_t w[4] = {hb[tt].x, hb[tt].y, hb[tt].z, hb[tt].w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              w[i] = nv > 2 * i + 1 ? w[i] : (nv > 2 * i ? (w[i] & 0xffffu) : 0u);
-            hb[tt] = make_uint4(w[0], w[1], w[2], w[3]);
-          }
-        } else {  // ragged tail of the array's last rows: guarded scalar loads (never past the row)
+        } else {  // ragged tail: guarded scalar loads (never past the row)
           uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
           for (int j = 0; j < 8; ++j)
@@ -179,7 +165,7 @@ k_logits_lone(
           a[s] = f32x4{0.f, 0.f, 0.f, 0.f};
           continue;
         }
-        if (s < ksf || (wide && s == kst - 1)) {
+        if (s < ksf) {
           if constexpr (A16) {
             a[s] = load4<XT>(xr + 16 * s);
           } else {  // 8-B aligned rows (an even row pitch: the reference's [N, 166]): two 8-B loads
@@ -187,12 +173,7 @@ k_logits_lone(
             const float2 u1 = *reinterpret_cast<const float2*>(xr + 16 * s + 2);
             a[s] = f32x4{u0.x, u0.y, u1.x, u1.y};
           }
-          if (s >= ksf) {  // the ragged k-step read whole: features >= F -> 0
-            const int nv = F - (16 * s + 4 * (opaque(lane0) >> 4));  // (not hoisted)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) a[s][u] = nv > u ? a[s][u] : 0.f;
-          }
-        } else if (s < kst) {  // ragged tail of the array's last rows: guarded scalar loads (never past the row)
+        } else if (s < kst) {  // ragged tail: guarded scalar loads (never past the row)
 #pragma unroll
           for (int u = 0; u < 4; ++u) a[s][u] = 16 * s + 4 * g + u < F ? xcvt(xr[16 * s + u]) : 0.f;
         } else {
@@ -343,32 +324,10 @@ k_logits_lone(
             for (int i = 0; i < 4; ++i) dst[i] = v[i];
           }
         };
-#ifdef GFD_AB_SLINE
-        if (qd >= 2 || !kH) {
-#endif
         if (qd < 2) put(sl + uint64_t(uint32_t(orow)) * uint32_t(lds) + 4 * qd);
         else put(tl + uint64_t(uint32_t(orow)) * uint32_t(ldt) + 4 * (qd - 2));
-#ifdef GFD_AB_SLINE
-        }
-#endif
       }
     }
-#ifdef GFD_AB_SLINE
-    // ablation (timing only): bf16 rows' s as the row's whole last 128-B line
-    if constexpr (kH) {
-      const int64_t orow = t * 16 + rl;
-      if (orow < rows) {
-        char* lb = const_cast<char*>(reinterpret_cast<const char*>(x)) + orow * ldx * 2 + 256 + 16 * g;
-        uint4 v5 = hb[5];
-        if (g == 1 || g == 2) {
-          const f32x4 sv4 = *reinterpret_cast<const f32x4*>(T + rl * kTP + 4 * (g - 1));
-          v5 = make_uint4(__float_as_uint(sv4[0]), __float_as_uint(sv4[1]), __float_as_uint(sv4[2]), __float_as_uint(sv4[3]));
-        }
-        __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&hb[4]), reinterpret_cast<f32x4*>(lb));
-        __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(&v5), reinterpret_cast<f32x4*>(lb + 64));
-      }
-    }
-#endif
     const int lone_i = lone ? 1 : 0;
     if (__builtin_expect(stats != nullptr, 0) && any_lone) {  // training (no dropout) only
 #pragma unroll
@@ -456,46 +415,34 @@ gfd_status launch_t(const void* x, int64_t rows, int F, int64_t ldx, const PackL
                     float* s, int lds, float* t, int ldt, float* xmax, float* out,
                     float* stats, const Epi& ep, hipStream_t stream) {
   const int64_t tiles = (rows + 15) / 16;
+  int64_t nb = (tiles + kLLWaves - 1) / kLLWaves;
+  const int64_t cap = int64_t(cu_count());  // resident blocks; grid-stride beyond
+  if (nb > cap) nb = cap;
   const uintptr_t xa = reinterpret_cast<uintptr_t>(x);
   const bool a16 = xa % 16 == 0 && (ldx * XT::kBytes) % 16 == 0;
   const bool k11 = F <= 176;
-  // the ragged last k-step read whole where the row pitch covers it: every
-  // tile but the last (which holds the array's last row) in the wide instance
-  const int KB = (F + 31) / 32, kst = (F + 15) / 16;
-  const bool widerow = (XT::kBytes == 2 ? 32 * KB : 16 * kst) <= ldx;
-  const int64_t t_wide = widerow ? tiles - 1 : 0;  // tiles [0, t_wide) wide
   // the epilogue (BN affine / ReLU / residual) and the folded head in their
   // own instances: the plain pass carries none of their code
   const bool epi = ep.ab != nullptr;
+#define GFD_LL(KS, HD, A) (epi ? &k_logits_lone<XT, KS, HD, A, true> : &k_logits_lone<XT, KS, HD, A, false>)
+  auto kern = a16 ? (ep.hout ? (k11 ? GFD_LL(11, true, true) : GFD_LL(12, true, true))
+                             : (k11 ? GFD_LL(11, false, true) : GFD_LL(12, false, true)))
+                  : (ep.hout ? (k11 ? GFD_LL(11, true, false) : GFD_LL(12, true, false))
+                             : (k11 ? GFD_LL(11, false, false) : GFD_LL(12, false, false)));
+#undef GFD_LL
   const size_t smem = sizeof(uint4) * 2 * kLKB * 5 * 64 + sizeof(float) * 2 * C +
                       sizeof(float) * kLLWaves * 16 * kTP;
+  if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
   const bool plain = XT::kBytes == 2;  // bf16: plain-order fragments (16-B loads)
-  for (int part = 0; part < 2; ++part) {
-    const bool wd = part == 0;
-    const int64_t tb = wd ? 0 : t_wide, te = wd ? t_wide : tiles;
-    if (te <= tb) continue;
-    int64_t nb = (te - tb + kLLWaves - 1) / kLLWaves;
-    const int64_t cap = int64_t(cu_count());  // resident blocks; grid-stride beyond
-    if (nb > cap) nb = cap;
-#define GFD_LL(KS, HD, A)                                                                    \
-  (wd ? (epi ? &k_logits_lone<XT, KS, HD, A, true, true> : &k_logits_lone<XT, KS, HD, A, false, true>) \
-      : (epi ? &k_logits_lone<XT, KS, HD, A, true, false> : &k_logits_lone<XT, KS, HD, A, false, false>))
-    auto kern = a16 ? (ep.hout ? (k11 ? GFD_LL(11, true, true) : GFD_LL(12, true, true))
-                               : (k11 ? GFD_LL(11, false, true) : GFD_LL(12, false, true)))
-                    : (ep.hout ? (k11 ? GFD_LL(11, true, false) : GFD_LL(12, true, false))
-                               : (k11 ? GFD_LL(11, false, false) : GFD_LL(12, false, false)));
-#undef GFD_LL
-    if (!ensure_lds(reinterpret_cast<const void*>(kern), smem)) return GFD_ERR_HIP;
-    kern<<<int(nb), kLLWaves * 64, smem, stream>>>(
-        static_cast<const typename XT::T*>(x), rows, F, ldx,
-        reinterpret_cast<const PackHeader*>(packed + L.hdr_off),
-        reinterpret_cast<const uint4*>(packed + (plain ? L.ush_off : L.uph_off)),
-        reinterpret_cast<const uint4*>(packed + (plain ? L.usl_off : L.upl_off)),
-        reinterpret_cast<const uint4*>(packed + (plain ? L.wbh_off : L.wph_off)),
-        reinterpret_cast<const uint4*>(packed + (plain ? L.wbl_off : L.wpl_off)), rowptr, bias, slope, s, lds, t, ldt,
-        xmax, out, stats, ep, tb, te);
-    GFD_LAUNCH_CHECK();
-  }
+  kern<<<int(nb), kLLWaves * 64, smem, stream>>>(
+      static_cast<const typename XT::T*>(x), rows, F, ldx,
+      reinterpret_cast<const PackHeader*>(packed + L.hdr_off),
+      reinterpret_cast<const uint4*>(packed + (plain ? L.ush_off : L.uph_off)),
+      reinterpret_cast<const uint4*>(packed + (plain ? L.usl_off : L.upl_off)),
+      reinterpret_cast<const uint4*>(packed + (plain ? L.wbh_off : L.wph_off)),
+      reinterpret_cast<const uint4*>(packed + (plain ? L.wbl_off : L.wpl_off)), rowptr, bias, slope, s, lds, t, ldt,
+      xmax, out, stats, ep);
+  GFD_LAUNCH_CHECK();
   return GFD_OK;
 }
 

@@ -327,10 +327,8 @@ def test_heavy_tailed_features_sharded(big):
 def test_nan_row_padding_and_last_row_at_allocation_end(dtype, F, ldx):
     """x with row pitch > F whose padding columns hold NaN, and whose last row
     ends exactly at the end of the allocation: lanes f >= F must read zeros
-    (buffer range check), never the padding or past the allocation.  Pitches
-    that cover the logits pass's padded last k-step (fp32 16 * ceil(F / 16),
-    bf16 32 * ceil(F / 32)) take its whole-vector tail loads (padding zeroed in
-    registers) on every tile but the last; 166 / 176 bf16 does not."""
+    (buffer range check), never the padding or past the allocation; fp32 and
+    bf16 rows, pitches with and without room for a whole padded k-step."""
     N = 5000
     ei, x, W, a_s, a_d, b = _small(N, 40000, F, seed=14)
     x = x.to(dtype)
