@@ -37,6 +37,9 @@ def main():
     p.add_argument("--exchange", choices=["halo", "halo1", "allgather"], default="halo")
     p.add_argument("--overlap", action="store_true",
                    help="light class on a second stream beside hubs -> general (bench --overlap)")
+    p.add_argument("--sync-standin", dest="async_standin", action="store_false",
+                   help="run the all-to-all's stand-in copy on the caller's stream (rounds 4-6 "
+                        "records) instead of a side stream joined at wait(), as RCCL's is")
     a = p.parse_args()
     from gfd import dist as gdist
     dev = torch.device("cuda", 0)
@@ -66,6 +69,7 @@ def main():
     needs = [gdist.halo_needs(g.col[int(rp[sp.dst_lo]):int(rp[sp.dst_hi])], sp) for sp in specs]
     cur = {}
     st_src = st_full[:, :8].contiguous()
+    side = torch.cuda.Stream()
 
     def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None,
                           async_op=False):
@@ -83,6 +87,21 @@ def main():
             plans = cur["plans"]
             pl = plans[cur["phase"] % len(plans)]
             cur["phase"] += 1
+            if async_op and a.async_standin:
+                # like RCCL's collective: on its own stream, after the pack that
+                # precedes it on the caller's stream; wait() joins it back
+                main = torch.cuda.current_stream()
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    gdist.rows_copy(st_src, pl.recv_rows, out, None)
+                done = torch.cuda.Event()
+                done.record(side)
+
+                class _Work:
+                    def wait(self):
+                        torch.cuda.current_stream().wait_event(done)
+                        return True
+                return _Work()
             gdist.rows_copy(st_src, pl.recv_rows, out, None)
 
         class _Done:
@@ -139,7 +158,13 @@ def main():
                       "note": "compute excludes the exchange stage; with --exchange halo that "
                               "stage's time here is the on-GPU part (gfd_rows_copy pack and "
                               "scatter, a device gather standing in for the all-to-all's "
-                              "transfer); the xGMI transfer needs the 8-GPU node",
+                              "transfer); the xGMI transfer needs the 8-GPU node.  standin "
+                              "'async': that gather runs on a side stream issued after the "
+                              "phase's pack and joined when the exchange stage waits, as RCCL's "
+                              "all-to-all is (phase 0's under the second half's logits pass, "
+                              "phase 1's exposed in the exchange stage); 'sync': on the "
+                              "rank's stream inside the logits stage (the round 4-6 records)",
+                      "standin": "async" if a.async_standin else "sync",
                       "ranks": ranks}))
 
 
