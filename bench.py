@@ -431,7 +431,7 @@ def stage_bytes(s, plan, esz, halo=None):
     g, F = s["graph"], s["F"]
     rp = s["shard"].rowptr
     deg = (rp[1:] - rp[:-1]).long()
-    light_b, lone_b = plan.classes()
+    light_b, lone_b = plan.classes(s["dtype"])   # (bf16 x: one message more is light)
     order = plan.row_order.long() if plan.row_order is not None else None
     sdeg = deg[order] if order is not None else deg
     hubs_mask = torch.zeros_like(sdeg, dtype=torch.bool)
@@ -554,7 +554,7 @@ def measure(args, dev, rank, world, config):
     esz = s["xbuf"].element_size()
     log(f"[bench] {config} rank {rank}/{world}: N={N} E={E} messages={s['graph'].num_messages} "
         f"shard=[{s['spec'].dst_lo},{s['spec'].dst_hi}) hubs={plan.num_hubs} "
-        f"chunks={plan.num_chunks} classes={plan.classes()} "
+        f"chunks={plan.num_chunks} classes={plan.classes(dtype)} "
         f"setup {time.perf_counter() - t_setup:.1f}s")
     if getattr(args, "legs_only", False) and config == "c4":
         return {"legs_only": True}, s, layer

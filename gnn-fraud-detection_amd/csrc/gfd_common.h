@@ -21,6 +21,15 @@ constexpr float kSoftmaxEps = 1e-16f;  // PyG utils.softmax denominator epsilon
 #define GFD_LIGHT_MAX 6
 #endif
 constexpr int kLightMax = GFD_LIGHT_MAX;
+// ... for bf16 rows: one message more.  Their light instance holds 7 rows a
+// slot spill-free (fp32 rows spill at 7), and the 7-message rows leave the
+// general tiles: C5 general + light -0.5 ms (profiles/r6s_light_bound_ab.txt).
+// The plan's class_split[3] is this bound's general / light boundary.
+#ifndef GFD_LIGHT_MAX_BF16
+#define GFD_LIGHT_MAX_BF16 7
+#endif
+constexpr int kLightMaxBf16 = GFD_LIGHT_MAX_BF16;
+static_assert(kLightMax <= 7 && kLightMaxBf16 <= 7, "light slots: at most 7 messages");
 // Messages of the largest destination of the "short light" sub-class: the
 // light tiles whose slots all have at most this many messages run a kernel
 // instance that prefetches only that many rows per slot, and spends the

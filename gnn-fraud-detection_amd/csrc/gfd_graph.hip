@@ -153,12 +153,14 @@ __global__ void k_order_keys(const int32_t* __restrict__ rowptr, int64_t n, int3
 // order -> hub_rank -> rowptr -> col chain of dependent loads in the tile kernel.
 // Also the class boundaries of the tile stage (max over slots of 1 + the slot
 // index of every hub / > kLightMax-message slot, of every hub / > 1-message
-// slot, and of every hub / > kLightLo-message slot): exact for any slot order.
+// slot, of every hub / > kLightLo-message slot, and of every hub /
+// > kLightMaxBf16-message slot -- bf16 rows' general / light boundary): exact
+// for any slot order.
 __global__ void k_slot_desc(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                             int64_t n, const int32_t* __restrict__ order,
                             const int32_t* __restrict__ hub_rank, int4* __restrict__ desc,
                             int32_t* __restrict__ cols8, int64_t* __restrict__ split) {
-  unsigned long long s_gen = 0, s_light = 0, s_short = 0;
+  unsigned long long s_gen = 0, s_light = 0, s_short = 0, s_gen16 = 0;
   for (int64_t s = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; s < n;
        s += int64_t(gridDim.x) * blockDim.x) {
     const int32_t i = order ? order[s] : int32_t(s);
@@ -172,17 +174,20 @@ __global__ void k_slot_desc(const int32_t* __restrict__ rowptr, const int32_t* _
     if (hr >= 0 || e - b > kLightMax) s_gen = (unsigned long long)(s + 1);
     if (hr >= 0 || e - b > 1) s_light = (unsigned long long)(s + 1);
     if (hr >= 0 || e - b > kLightLo) s_short = (unsigned long long)(s + 1);
+    if (hr >= 0 || e - b > kLightMaxBf16) s_gen16 = (unsigned long long)(s + 1);
   }
   if (split) {
     for (int o = 32; o > 0; o >>= 1) {
       s_gen = max(s_gen, (unsigned long long)__shfl_xor((long long)s_gen, o));
       s_light = max(s_light, (unsigned long long)__shfl_xor((long long)s_light, o));
       s_short = max(s_short, (unsigned long long)__shfl_xor((long long)s_short, o));
+      s_gen16 = max(s_gen16, (unsigned long long)__shfl_xor((long long)s_gen16, o));
     }
     if ((threadIdx.x & 63) == 0) {
       if (s_gen) atomicMax(reinterpret_cast<unsigned long long*>(split), s_gen);
       if (s_light) atomicMax(reinterpret_cast<unsigned long long*>(split + 1), s_light);
       if (s_short) atomicMax(reinterpret_cast<unsigned long long*>(split + 2), s_short);
+      if (s_gen16) atomicMax(reinterpret_cast<unsigned long long*>(split + 3), s_gen16);
     }
   }
 }
@@ -236,7 +241,7 @@ gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t n,
                          int32_t* slot_cols, int64_t* class_split, gfd_stream_t stream_) {
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   if (n <= 0 || !rowptr || !desc || (slot_cols && !col)) return GFD_ERR_ARGUMENT;
-  if (class_split) GFD_HIP_CHECK(hipMemsetAsync(class_split, 0, 3 * sizeof(int64_t), stream));
+  if (class_split) GFD_HIP_CHECK(hipMemsetAsync(class_split, 0, 4 * sizeof(int64_t), stream));
   k_slot_desc<<<grid_for(n), kBlock, 0, stream>>>(rowptr, col, n, order, hub_rank,
                                                   reinterpret_cast<int4*>(desc), slot_cols,
                                                   class_split);
@@ -256,7 +261,7 @@ const char* gfd_status_string(gfd_status s) {
   }
 }
 
-int gfd_abi_version(void) { return 8; }
+int gfd_abi_version(void) { return 9; }
 
 static size_t csr_layout(int64_t E, int64_t N, size_t* sort_tmp_out, size_t* scan_tmp_out) {
   size_t sort_tmp = 0, scan_tmp = 0;

@@ -129,7 +129,7 @@ constexpr int ap_of() {
 template <int LIGHT, typename XT, bool PR = false>
 constexpr int nl_of() {
   return LIGHT == 2 ? kLightLo
-       : LIGHT ? kLightMax
+       : LIGHT ? (XT::kBytes == 2 ? kLightMaxBf16 : kLightMax)
        : (XT::kBytes == 2 ? (PR ? GFD_GENERAL_NL_BF16P : GFD_GENERAL_NL_BF16) : GFD_GENERAL_NL_F32);
 }
 
@@ -491,15 +491,17 @@ __global__ void __launch_bounds__(kSWaves * 64, 2) k_stream(
   const int r0 = 2 * wave, r1 = r0 + 1;
   const int64_t G = gridDim.x;
   const int64_t t0 = blockIdx.x;
-  // general tiles: [0, ceil(split[0] / 16)), every tile without a split;
-  // light tiles: [ceil(split[0] / 16), ceil(split[2] / 16)); short light
+  // general tiles: [0, ceil(split[g] / 16)), every tile without a split;
+  // light tiles: [ceil(split[g] / 16), ceil(split[2] / 16)); short light
   // tiles: [ceil(split[2] / 16), ceil(split[1] / 16)) (to_end: up to the last
-  // tile, when k_lone does not run); this block takes tiles t0 + v G
+  // tile, when k_lone does not run); this block takes tiles t0 + v G.  g = 0
+  // (light bound kLightMax) for fp32 rows, 3 (kLightMaxBf16) for bf16 rows
+  constexpr int kG = XT::kBytes == 2 ? 3 : 0;
   const int64_t all = (num_dst + kTile - 1) / kTile;
-  const int64_t tb = LIGHT ? (split[LIGHT == 2 ? 2 : 0] + kTile - 1) / kTile : 0;
+  const int64_t tb = LIGHT ? (split[LIGHT == 2 ? 2 : kG] + kTile - 1) / kTile : 0;
   const int64_t te = LIGHT == 2 ? ((to_end ? num_dst : split[1]) + kTile - 1) / kTile
                    : LIGHT ? (split[2] + kTile - 1) / kTile
-                           : (split ? (split[0] + kTile - 1) / kTile : all);
+                           : (split ? (split[kG] + kTile - 1) / kTile : all);
   const int64_t nv = t0 < te - tb ? (te - tb - 1 - t0) / G + 1 : 0;
   // light, not to the end: the slots of the last tile past split[1] are lone
   // rows another kernel writes -- taken as empty here

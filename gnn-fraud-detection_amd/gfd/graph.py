@@ -105,12 +105,13 @@ class Plan:
         ck = self.hub_chunk.view(-1, 4)
         return int((ck[:, 2] - ck[:, 1]).sum().item())
 
-    def classes(self) -> Tuple[int, int]:
-        """(first light slot, first lone slot) on the host (syncs)."""
+    def classes(self, dtype: Optional[torch.dtype] = None) -> Tuple[int, int]:
+        """(first light slot, first lone slot) on the host (syncs).  The light
+        class of bf16 rows takes one message more (``class_split[3]``: ABI 9)."""
         if self.class_split is None:
             return self.num_dst, self.num_dst
-        a, b = self.class_split.tolist()[:2]
-        return int(a), int(b)
+        sp = self.class_split.tolist()
+        return int(sp[3] if dtype == torch.bfloat16 else sp[0]), int(sp[1])
 
 
 def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THRESHOLD,
@@ -140,7 +141,7 @@ def build_plan(rowptr: torch.Tensor, num_messages: int, threshold: int = HUB_THR
         slot_desc = torch.empty(4 * n, dtype=torch.int32, device=dev)
         if col is not None:
             slot_cols = torch.empty(8 * n, dtype=torch.int32, device=dev)
-            class_split = torch.empty(3, dtype=torch.int64, device=dev)
+            class_split = torch.empty(4, dtype=torch.int64, device=dev)
         _lib.call("gfd_plan_desc", rowptr.data_ptr(), _lib.ptr(col), n, _lib.ptr(row_order),
                   hub_rank.data_ptr() if nh > 0 else None, slot_desc.data_ptr(),
                   _lib.ptr(slot_cols), _lib.ptr(class_split), stream)

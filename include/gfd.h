@@ -138,15 +138,18 @@ gfd_status gfd_plan_order(const int32_t* rowptr, int64_t num_dst, int32_t cap, i
  * tile slot s (row = order[s], or s when order is NULL; hub_rank -1 when
  * NULL) and, when slot_cols is not NULL, slot_cols[8*s + k] = col[min(e_begin
  * + k, e_end - 1)] (the first 8 sources, prefetched one tile ahead).
- * class_split (nullable, device int64[3]; ABI 8: was [2]) receives the slot
- * class boundaries the forward's tile stage schedules by: class_split[0] = 1 +
- * the last slot that is a hub or has more than 6 messages, class_split[1] = 1 +
- * the last slot that is a hub or has more than 1 message, class_split[2] = 1 +
- * the last slot that is a hub or has more than 3 messages (0 when there is
- * none).  Slots past class_split[0] are "light" (2..6 messages), slots past
- * class_split[2] "short light" (at most 3: their own kernel instance), slots
- * past class_split[1] "lone" (self loop only).  Correct for ANY order: an order
- * that is not degree-sorted only moves the boundaries towards num_dst. */
+ * class_split (nullable, device int64[4]; ABI 9 -- [3] in ABI 8, [2] before)
+ * receives the slot class boundaries the forward's tile stage schedules by:
+ * class_split[0] = 1 + the last slot that is a hub or has more than 6
+ * messages, class_split[1] = 1 + the last slot that is a hub or has more than
+ * 1 message, class_split[2] = 1 + the last slot that is a hub or has more
+ * than 3 messages, class_split[3] = 1 + the last slot that is a hub or has
+ * more than 7 messages (0 when there is none).  Slots past class_split[0]
+ * (fp32 x) or class_split[3] (bf16 x) are "light" (2..6 / 2..7 messages),
+ * slots past class_split[2] "short light" (at most 3: their own kernel
+ * instance), slots past class_split[1] "lone" (self loop only).  Correct for
+ * ANY order: an order that is not degree-sorted only moves the boundaries
+ * towards num_dst. */
 gfd_status gfd_plan_desc(const int32_t* rowptr, const int32_t* col, int64_t num_dst,
                          const int32_t* order, const int32_t* hub_rank, int32_t* desc,
                          int32_t* slot_cols, int64_t* class_split, gfd_stream_t stream);
@@ -236,7 +239,7 @@ typedef struct gfd_plan {
   const int32_t* hub_chunk;     /* [4*num_chunks] {hub, e_begin, e_end, dst}           */
   const int32_t* hub_chunk_ptr; /* [num_hubs + 1]                                      */
   const int32_t* hub_dst;       /* [num_hubs]                                          */
-  const int64_t* class_split;   /* [3] gfd_plan_desc class boundaries, or NULL: every  */
+  const int64_t* class_split;   /* [4] gfd_plan_desc class boundaries, or NULL: every  */
                                 /* slot runs the general tile kernel                   */
   int64_t num_hubs;
   int64_t num_chunks;
@@ -257,8 +260,8 @@ size_t gfd_gat_fwd_workspace_size(int64_t num_nodes, int64_t num_dst, int in_fea
  * GFD_STAGE_TILES (the tile kernels of every destination class, reading the
  * merged hub rows from ws) or GFD_STAGE_ALL; split calls must pass the same ws.
  * The tile stage schedules destinations by the plan's classes: general (hub
- * rows, 7+ messages), light (2..6 messages, GFD_LIGHT_MAX in gfd_common.h),
- * lone (self loop only). */
+ * rows, 7+ messages; bf16 x: 8+), light (2..6 messages, GFD_LIGHT_MAX in
+ * gfd_common.h; bf16 x: 2..7, GFD_LIGHT_MAX_BF16), lone (self loop only). */
 #define GFD_STAGE_HUBS 1
 #define GFD_STAGE_TILES 2
 #define GFD_STAGE_ALL 3

@@ -58,7 +58,7 @@ def test_build_id_is_the_source_hash(lib):
 
 
 def test_version_and_status_strings(lib):
-    assert lib.gfd_abi_version() == 8
+    assert lib.gfd_abi_version() == 9
     assert b"range" in lib.gfd_status_string(2)
     assert lib.gfd_status_string(99) == b"unknown status"
 

@@ -29,7 +29,7 @@ def _sample(layer, s, extra=()):
     plan = layer.plan
     N = g.num_nodes
     deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
-    light_b, lone_b = plan.classes()
+    light_b, lone_b = plan.classes(s["x"].dtype)
     order = plan.row_order.long()
     gen = torch.Generator(device=DEV).manual_seed(3)
     pick = [torch.topk(deg, 16).indices,                              # largest hubs

@@ -54,7 +54,7 @@ def _c5_sample(layer, s):
     plan = layer.plan
     N = g.num_nodes
     deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
-    light_b, lone_b = plan.classes()
+    light_b, lone_b = plan.classes(s["x"].dtype)
     order = plan.row_order.long()
     gen = torch.Generator(device=DEV).manual_seed(5)
     by_deg = torch.argsort(deg, descending=True)
@@ -88,8 +88,9 @@ def test_c5_full_size_sampled_parity(c5):
     assert s["ldx"] == 184 and s["x"].dtype == torch.bfloat16
     assert s["xbuf"].numel() > 2 ** 32                      # element indices past 2^32
     layer = bench.Layer(s, DEV, 1)
-    light_b, lone_b = layer.plan.classes()
+    light_b, lone_b = layer.plan.classes(torch.bfloat16)
     assert 0 < light_b < lone_b < s["graph"].num_nodes
+    assert light_b < layer.plan.classes()[0]                # bf16: the 7-message rows are light
     assert layer.plan.num_chunks > 500_000                   # the C5 hub-chunk regime (384-message chunks)
     layer.step()
     torch.cuda.synchronize()
